@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""bench.py -- SOS team-reduction path (shmem_<T>_<op>_reduce) on MI355X.
+
+Metric (BASELINE.json): GiB/s of the device-resident sum_reduce combine,
+nreduce = 128Mi fp32, at 1/2/4/8 GPUs (one PE per GPU).
+
+  N = 1 : one step = one local combine inout = inout + in over 128Mi fp32 resident in
+          HBM (sosx_combine, the device shmem_internal_reduce_local,
+          src/shmem_internal_op.h:305-339).  At PE_size 1 the reference API itself
+          only copies (src/collectives.c:664-668), so the combine kernel is the
+          single-GPU workload.
+  N > 1 : one step = one shmem_float_sum_reduce(SHMEM_TEAM_WORLD, dest, src, 128Mi)
+          over N PEs (weak scaling: every PE reduces its own 128Mi vector).
+  value = sum over PEs of nreduce*sizeof(T) bytes reduced per step / step time, GiB/s.
+
+One JSON line on rank 0's stdout.  `roofline` is the dominant kernel's algorithmic
+HBM bytes per launch / its HIP-event-timed mean duration; `cpu_baseline` is the CPU
+restatement of reduce_local (oracle/sos_oracle.c, gcc -O2, one core) on a bounded
+sample of the same workload.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--variants] [--no-cpu]
+       torchrun --nproc-per-node N bench.py --gpus N   (N > 1)
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+GiB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
+SEED = 0x5EED
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--n", type=int, default=128 << 20, help="nreduce (elements)")
+    p.add_argument("--dtype", default="float")
+    p.add_argument("--op", default="sum")
+    p.add_argument("--alg", default=os.environ.get("SHMEM_REDUCE_ALGORITHM", "auto"))
+    p.add_argument("--variant", type=int, default=0, help="combine kernel variant")
+    p.add_argument("--variants", action="store_true", help="A/B every combine variant")
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-pmc", action="store_true")
+    p.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
+    return p.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ----------------------------------------------------------------------------------
+# N = 1: the local combine
+# ----------------------------------------------------------------------------------
+def combine_setup(args, torch, S):
+    from sos_amd import _lib as L
+    dt = L.dtype_id(args.dtype)
+    es = L.dtype_size(dt)
+    nbytes = args.n * es
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    dist = L.DIST_PROD if args.op == "prod" else L.DIST_UNIFORM
+    L.fill(dt, dist, SEED, 0, a.data_ptr(), args.n, 0, S)
+    L.fill(dt, dist, SEED, 1, b.data_ptr(), args.n, 0, S)
+    torch.cuda.synchronize()
+    return L, dt, es, a, b
+
+
+def run_combine(args, torch):
+    stream = torch.cuda.current_stream()
+    S = stream.cuda_stream
+    L, dt, es, a, b = combine_setup(args, torch, S)
+    lib = L.lib()
+    op = L.op_id(args.op)
+    lib.sosx_set_combine_variant(args.variant)
+    launch = lambda: L.combine(op, dt, a.data_ptr(), b.data_ptr(), args.n, S)  # noqa: E731
+
+    if args.child_pmc:  # profiled child: a few launches only
+        for _ in range(args.warmup + args.steps):
+            launch()
+        torch.cuda.synchronize()
+        return None
+
+    if args.variants:
+        variants_ab(args, torch, L, launch)
+
+    for _ in range(args.warmup):
+        launch()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        launch()
+        e.record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    kern_ms = sorted(s.elapsed_time(e) for s, e in ev)
+    mean_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+    step_s = (t1 - t0) / args.steps
+    payload = args.n * es
+    algo_bytes = 3 * payload  # read in, read inout, write inout
+    achieved = algo_bytes / mean_kern_s / 1e9
+    res = {
+        "metric": "GiB/s device-resident sum_reduce combine, nreduce=128Mi fp32; 1/2/4/8 GPU",
+        "value": round(payload / step_s / GiB, 3),
+        "unit": "GiB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": {"float": "f32", "double": "f64"}.get(args.dtype, args.dtype),
+        "data": "synthetic (splitmix64 counter hash, SURVEY.md 8(d)), resident in HBM",
+        "config": {"workload": f"shmem_{args.dtype}_{args.op}_reduce local combine "
+                               f"(reduce_local inout OP= in), nreduce={args.n}, 1 PE",
+                   "nreduce": args.n, "op": args.op, "type": args.dtype,
+                   "kernel_variant": lib.sosx_combine_variant_name(args.variant).decode()},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None,
+                     "kernel": "sos::k_combine3", "algorithmic_bytes_per_launch": algo_bytes,
+                     "mean_kernel_ms": round(mean_kern_s * 1e3, 5),
+                     "median_kernel_ms": round(kern_ms[len(kern_ms) // 2], 5)},
+    }
+    return res
+
+
+def variants_ab(args, torch, L, launch):
+    """Interleaved A/B of every combine variant in one process (guide rule 24)."""
+    lib = L.lib()
+    nv = lib.sosx_num_combine_variants()
+    stream = torch.cuda.current_stream()
+    es = L.dtype_size(L.dtype_id(args.dtype))
+    results = {v: [] for v in range(nv)}
+    for r in range(args.rounds):
+        for v in range(nv):
+            lib.sosx_set_combine_variant(v)
+            for _ in range(3):
+                launch()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            for _ in range(20):
+                launch()
+            e.record(stream)
+            torch.cuda.synchronize()
+            results[v].append(s.elapsed_time(e) / 20)
+    log(f"{'variant':>18} {'median ms':>10} {'min ms':>9} {'HBM GB/s(3 streams)':>20}")
+    for v in range(nv):
+        ms = sorted(results[v])
+        med = ms[len(ms) // 2]
+        gbs = 3 * args.n * es / (med / 1e3) / 1e9
+        log(f"{lib.sosx_combine_variant_name(v).decode():>18} {med:10.4f} {ms[0]:9.4f} {gbs:20.1f}")
+    lib.sosx_set_combine_variant(args.variant)
+
+
+# ----------------------------------------------------------------------------------
+# PMC traffic: rocprofv3 --pmc pass(es) over a child run of this script
+# ----------------------------------------------------------------------------------
+def pmc_traffic(args):
+    """HBM bytes per combine launch from TCC FETCH_SIZE/WRITE_SIZE (KB units).
+    gfx950: FETCH_SIZE counts half the bytes of a 16-B/lane streaming read
+    (MI355X_MICROARCH.md, HBM), so reads = 2*FETCH_SIZE.  Separate passes, since
+    FETCH_SIZE and WRITE_SIZE do not fit one TCC pass."""
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="sos_pmc_")
+        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__), "--child-pmc", "--steps", "3",
+               "--warmup", "1", "--n", str(args.n), "--dtype", args.dtype, "--op", args.op,
+               "--variant", str(args.variant)]
+        try:
+            subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL, env=dict(os.environ, TMPDIR="/tmp"))
+        except Exception as exc:  # noqa: BLE001 - a profiler failure must not kill the bench
+            return None, f"rocprofv3 {ctr} pass failed: {exc}"
+        rows = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if "k_combine3" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                        rows.append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not rows:
+            return None, f"no {ctr} rows"
+        vals[ctr] = sum(rows) / len(rows)
+    traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+    return traffic, vals
+
+
+# ----------------------------------------------------------------------------------
+# CPU baseline: the restated reduce_local on one host core
+# ----------------------------------------------------------------------------------
+def cpu_baseline(args):
+    import numpy as np
+    from oracle import oracle as O
+    from sos_amd import _lib as L
+    dt = L.dtype_id(args.dtype)
+    dist = L.DIST_PROD if args.op == "prod" else L.DIST_UNIFORM
+    inout = O.fill(dt, dist, SEED, 0, args.n)
+    inp = O.fill(dt, dist, SEED, 1, args.n)
+    op = L.op_id(args.op)
+    t = O.time_reduce_local(op, dt, inp, inout, 1)  # warm-up + per-rep estimate
+    reps = max(1, int(args.cpu_seconds / max(t, 1e-6)))
+    t = O.time_reduce_local(op, dt, inp, inout, reps)
+    es = inout.itemsize
+    del inout, inp
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    _ = np
+    return {"value": round(reps * args.n * es / t / GiB, 3), "unit": "GiB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"reduce_local({args.op}, {args.dtype}) n={args.n} x {reps} reps, "
+                      f"{t:.1f} s, oracle/sos_oracle.c gcc -O2 (SOS default flags), 1 thread; "
+                      f"host: {model}, nproc={os.cpu_count()}"}
+
+
+# ----------------------------------------------------------------------------------
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus and not args.child_pmc:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if world > 1:
+        from sos_amd import team_bench
+        return team_bench.main(args, torch)
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    res = run_combine(args, torch)
+    if res is None:
+        return 0
+    if rank == 0 and not args.no_pmc:
+        traffic, info = pmc_traffic(args)
+        if traffic is not None:
+            res["roofline"]["traffic"] = round(traffic)
+            res["roofline"]["traffic_note"] = ("(2*FETCH_SIZE + WRITE_SIZE)*1024 B per launch, "
+                                               "rocprofv3 --pmc, gfx950 FETCH_SIZE halving corrected")
+        else:
+            res["roofline"]["traffic_note"] = str(info)
+    if rank == 0 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(args)
+    print(json.dumps(res), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,66 @@
+/*
+ * shmemx.h -- extensions of the MI355X SOS reduction path.
+ *
+ *   shmemx_heap_create      SOS's external-heap hook (src/symmetric_heap_c.c:439-464,
+ *                           mpp/shmemx-def.h:25-26) with a HIP device type, so a
+ *                           device (HBM) region is symmetric memory the reductions
+ *                           can run on without host staging.
+ *   shmemx_malloc_device    collective symmetric allocation in HBM.
+ *   shmemx_reduce_local     the local combine (shmem_internal_reduce_local,
+ *                           src/shmem_internal_op.h:305-339) on device memory.
+ *   shmemx_init_attr /      bootstrap with an RCCL unique id obtained out of band
+ *   shmemx_get_unique_id    (e.g. broadcast by torch.distributed), instead of the
+ *                           built-in TCP bootstrap of shmem_init().
+ *   shmemx_set_stream       run the collectives on the caller's HIP stream.
+ */
+#ifndef SHMEMX_H
+#define SHMEMX_H
+
+#include <stddef.h>
+
+#include "shmem.h"
+#include "sosx.h"
+
+#define SHMEMX_EXTERNAL_HEAP_ZE   0
+#define SHMEMX_EXTERNAL_HEAP_CUDA 1
+#define SHMEMX_EXTERNAL_HEAP_HIP  2   /* this build: HBM of the PE's MI355X */
+
+#define SHMEMX_UNIQUE_ID_BYTES 128    /* NCCL_UNIQUE_ID_BYTES */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+SHMEM_FUNCTION_ATTRIBUTES void shmemx_heap_create(void *base, size_t size, int device_type,
+                                                  int device_index);
+SHMEM_FUNCTION_ATTRIBUTES void *shmemx_malloc_device(size_t size);
+SHMEM_FUNCTION_ATTRIBUTES void shmemx_free_device(void *ptr);
+
+SHMEM_FUNCTION_ATTRIBUTES int shmemx_get_unique_id(void *uid, size_t len);
+SHMEM_FUNCTION_ATTRIBUTES int shmemx_init_attr(int my_pe, int n_pes, const void *uid, size_t len);
+
+SHMEM_FUNCTION_ATTRIBUTES void shmemx_set_stream(void *hip_stream);
+SHMEM_FUNCTION_ATTRIBUTES void *shmemx_get_stream(void);
+SHMEM_FUNCTION_ATTRIBUTES int shmemx_get_device(void);
+
+/* inout[i] = inout[i] OP in[i] on device memory; op/datatype are SOS's internal
+ * enums (SOSX_OP_*, SOSX_DT_*).  Asynchronous on the library stream. */
+SHMEM_FUNCTION_ATTRIBUTES int shmemx_reduce_local(int op, int datatype, size_t count,
+                                                  const void *in, void *inout);
+
+/* Reduction algorithm control, as SHMEM_REDUCE_ALGORITHM (src/collectives.c:195-210):
+ * SOSX_ALG_AUTO / _RECDBL / _RING / _RECHALVING / _RECDBL_DIRECT. */
+SHMEM_FUNCTION_ATTRIBUTES int shmemx_set_reduce_algorithm(int alg);
+
+/* Single-GPU loopback team (tests/validation): run the SOS team reduction of P
+ * simulated PEs whose source/target buffers all live on this device, with the same
+ * per-PE plans the RCCL executor runs and device-to-device copies as the transport. */
+SHMEM_FUNCTION_ATTRIBUTES int sosx_loopback_allreduce(int alg, int P, int op, int datatype,
+                                                      void *const *srcs, void *const *dsts,
+                                                      size_t count, void *stream);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* SHMEMX_H */

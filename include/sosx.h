@@ -1,0 +1,139 @@
+/*
+ * sosx.h -- the thin C ABI between the host side of the SOS reduction path and the
+ * hand-written gfx950 (MI355X) HIP kernels in libsos_amd.so.
+ *
+ * Plain C types only: pointers, sizes, ints.  `stream` is a hipStream_t passed as
+ * void* (NULL = the library's own per-PE stream).  Every entry point returns an int
+ * status (SOSX_OK or a negative SOSX_ERR_*); the shmem.h API layer turns non-zero
+ * statuses into an abort, as SOS's RAISE_ERROR_MSG does (src/shmem_internal.h:124-128).
+ *
+ * Enum values are SOS's own, so an SOS maintainer can pass them through unchanged:
+ *   op     : shm_internal_op_t        (src/transport_none.h:25-33)
+ *   dtype  : shm_internal_datatype_t  (src/transport.h:19-49)
+ */
+#ifndef SOSX_H
+#define SOSX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------- */
+#define SOSX_OK                0
+#define SOSX_ERR_DTYPE        (-1)  /* "invalid data type" (src/shmem_internal_op.h:335) */
+#define SOSX_ERR_OP           (-2)  /* "unsupported reduction on <type>" (:245,:260,:285) */
+#define SOSX_ERR_ARG          (-3)  /* bad pointer/count/team argument */
+#define SOSX_ERR_HIP          (-4)  /* a HIP runtime call failed */
+#define SOSX_ERR_RCCL         (-5)  /* an RCCL call failed */
+#define SOSX_ERR_UNSUPPORTED  (-6)  /* valid in SOS, not available on this device path */
+#define SOSX_ERR_STATE        (-7)  /* library not initialised / already initialised */
+
+/* ---- shm_internal_op_t (src/transport_none.h:25-33) ----------------------- */
+#define SOSX_OP_BAND 0
+#define SOSX_OP_BOR  1
+#define SOSX_OP_BXOR 2
+#define SOSX_OP_MIN  3
+#define SOSX_OP_MAX  4
+#define SOSX_OP_SUM  5
+#define SOSX_OP_PROD 6
+
+/* ---- shm_internal_datatype_t (src/transport.h:19-49) ---------------------- */
+#define SOSX_DT_SIGNED_BYTE     0
+#define SOSX_DT_CHAR            1
+#define SOSX_DT_SCHAR           2
+#define SOSX_DT_SHORT           3
+#define SOSX_DT_INT             4
+#define SOSX_DT_LONG            5
+#define SOSX_DT_LONG_LONG       6
+#define SOSX_DT_FORTRAN_INTEGER 7
+#define SOSX_DT_INT8            8
+#define SOSX_DT_INT16           9
+#define SOSX_DT_INT32          10
+#define SOSX_DT_INT64          11
+#define SOSX_DT_PTRDIFF_T      12
+#define SOSX_DT_UCHAR          13
+#define SOSX_DT_USHORT         14
+#define SOSX_DT_UINT           15
+#define SOSX_DT_ULONG          16
+#define SOSX_DT_ULONG_LONG     17
+#define SOSX_DT_UINT8          18
+#define SOSX_DT_UINT16         19
+#define SOSX_DT_UINT32         20
+#define SOSX_DT_UINT64         21
+#define SOSX_DT_SIZE_T         22
+#define SOSX_DT_FLOAT          23
+#define SOSX_DT_DOUBLE         24
+#define SOSX_DT_LONG_DOUBLE    25
+#define SOSX_DT_FLOAT_COMPLEX  26
+#define SOSX_DT_DOUBLE_COMPLEX 27
+#define SOSX_DT_COUNT          28
+
+/* ---- fold orders (how a P-input element is combined) ----------------------- */
+#define SOSX_ORDER_LINEAR 0  /* acc = in[0]; acc = acc OP in[k], k = 1..P-1 (ring fold) */
+#define SOSX_ORDER_TREE   1  /* recdbl_sw butterfly tree (src/collectives.c:905-963)   */
+
+/* ---- reduction algorithms (SHMEM_REDUCE_ALGORITHM, src/collectives.c:195-210) */
+#define SOSX_ALG_AUTO       0  /* SOS AUTO without NIC atomics (src/shmem_collectives.h:180-199) */
+#define SOSX_ALG_RECDBL     1  /* butterfly, full vector per step (src/collectives.c:850-984)    */
+#define SOSX_ALG_RING       2  /* ring fold order (src/collectives.c:647-764), direct exchange  */
+#define SOSX_ALG_RECHALVING 3  /* recursive halving + doubling, recdbl_sw tree, pairwise xGMI  */
+#define SOSX_ALG_RECDBL_DIRECT 4 /* recdbl_sw tree evaluated by the owner after a direct exchange */
+
+/* ---- synthetic input distributions ------------------------ */
+#define SOSX_DIST_UNIFORM 0  /* fp: uniform [-1,1); ints: full-range random bits      */
+#define SOSX_DIST_PROD    1  /* fp: [0.5,2) (complex: +-[0.5,1) parts); ints: [-3,3]   */
+
+/* Size in bytes of the C type behind `dtype` on x86-64/LP64, 0 if not reducible. */
+size_t sosx_dtype_size(int dtype);
+
+/* 0 if (op, dtype) is a valid reduce_local combination, else SOSX_ERR_DTYPE/OP. */
+int sosx_check_op(int op, int dtype);
+
+/*
+ * inout[i] = inout[i] OP in[i], i < count, on device memory, async on `stream`.
+ * Device replacement for shmem_internal_reduce_local (src/shmem_internal_op.h:305-339):
+ * same op/dtype enums, same operand order (left = inout), same per-type semantics.
+ * Unlike the reference, `count` is size_t (the reference's int truncates at 2^31).
+ */
+int sosx_combine(int op, int dtype, void *inout, const void *in, size_t count, void *stream);
+
+/* out[i] = a[i] OP b[i]; `out` may alias `a` (then this is sosx_combine). */
+int sosx_combine3(int op, int dtype, void *out, const void *a, const void *b, size_t count,
+                  void *stream);
+
+/*
+ * out[i] = fold_{k<nin}(ins[k][i]) in the given SOSX_ORDER_*; `out` may alias ins[0].
+ * nin <= SOSX_MAX_FOLD.  This is the fused P-way combine used by the team schedules.
+ */
+#define SOSX_MAX_FOLD 64
+int sosx_fold(int op, int dtype, int order, void *out, const void *const *ins, int nin,
+              size_t count, void *stream);
+
+/* Fill `count` elements of device buffer dst with the synthetic input of PE `pe`,
+ * element indices [index0, index0 + count).  Bit-identical to the CPU generator
+ * (tests/ and bench.py use oracle/sos_oracle.c's oracle_fill). */
+int sosx_fill(int dtype, int dist, uint64_t seed, int pe, void *dst, size_t count,
+              size_t index0, void *stream);
+
+/* Bitwise comparison of two device buffers; *mismatches receives the number of
+ * differing elements (elements of `elem_size` bytes).  Synchronous. */
+int sosx_count_mismatch(const void *a, const void *b, size_t count, size_t elem_size,
+                        unsigned long long *mismatches, void *stream);
+
+/* Kernel variant selection for the hot fp32/generic combine (bench/tuning only):
+ * returns the previous variant.  0 = default. */
+int sosx_set_combine_variant(int variant);
+int sosx_num_combine_variants(void);
+const char *sosx_combine_variant_name(int variant);
+
+/* Library / build identification. */
+const char *sosx_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SOSX_H */

@@ -1,0 +1,327 @@
+/*
+ * sos_oracle.c -- CPU restatement of the Sandia OpenSHMEM (SOS v1.5.3) team-reduction
+ * path, used ONLY as test infrastructure.
+ *
+ *   *** TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's
+ *   *** cpu_baseline leg may load this library, and only as the checker / the timed
+ *   *** CPU baseline.  The product (sos_amd/libsos_amd.so) never links or calls it.
+ *
+ * Parity pinning: the reference's combine header cannot be compiled from its own
+ * sources here (src/shmem_internal_op.h -> transport.h -> transport_none.h ->
+ * shmem_internal.h needs configure-generated config.h and m4-generated shmemx.h), so
+ * oracle/_ref is not built.  This file restates the same C expressions, compiled by
+ * the same gcc with SOS's default flags (-std=gnu11 -O2), and is pinned by the
+ * known-answer tests listed in SURVEY.md 8(c) (examples/pi_reduce.c outputs) and the
+ * man/shmem_reductions.3 example, evaluated in tests/test_oracle_kat.py.
+ *
+ * Contents
+ *   oracle_reduce_local  -- src/shmem_internal_op.h:305-339 (+ FUNC_OP_CREATE :23-33,
+ *                           op macros :37-43, dtype classes :225-303)
+ *   oracle_ring          -- src/collectives.c:647-764 (P PEs simulated in one process)
+ *   oracle_recdbl        -- src/collectives.c:850-984 (P PEs simulated in one process)
+ *   oracle_*_time        -- single-core timing helpers for bench.py's cpu_baseline
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <complex.h>
+
+/* shm_internal_op_t, src/transport_none.h:25-33 */
+enum { O_BAND = 0, O_BOR, O_BXOR, O_MIN, O_MAX, O_SUM, O_PROD };
+
+/* shm_internal_datatype_t, src/transport.h:19-49 */
+enum {
+    D_SIGNED_BYTE = 0, D_CHAR, D_SCHAR, D_SHORT, D_INT, D_LONG, D_LONG_LONG,
+    D_FORTRAN_INTEGER, D_INT8, D_INT16, D_INT32, D_INT64, D_PTRDIFF_T, D_UCHAR,
+    D_USHORT, D_UINT, D_ULONG, D_ULONG_LONG, D_UINT8, D_UINT16, D_UINT32, D_UINT64,
+    D_SIZE_T, D_FLOAT, D_DOUBLE, D_LONG_DOUBLE, D_FLOAT_COMPLEX, D_DOUBLE_COMPLEX,
+    D_COUNT
+};
+
+/* Elementwise loop: out = calc(out, in), left operand is the in/out buffer
+ * (src/shmem_internal_op.h:23-33). */
+#define O_MAXF(a, b) ((a) > (b) ? (a) : (b))
+#define O_MINF(a, b) ((a) < (b) ? (a) : (b))
+#define O_SUMF(a, b) ((a) + (b))
+#define O_PRODF(a, b) ((a) * (b))
+#define O_ANDF(a, b) ((a) & (b))
+#define O_ORF(a, b) ((a) | (b))
+#define O_XORF(a, b) ((a) ^ (b))
+
+#define O_LOOP(ctype, calc)                                           \
+    do {                                                              \
+        ctype *o_ = (ctype *) inout;                                  \
+        const ctype *i_ = (const ctype *) in;                         \
+        for (int k_ = 0; k_ < count; ++k_) o_[k_] = calc(o_[k_], i_[k_]); \
+    } while (0)
+
+/* op classes of src/shmem_internal_op.h:225-303 */
+#define O_CASE_FP(ctype)                                   \
+    switch (op) {                                          \
+        case O_MIN: O_LOOP(ctype, O_MINF); return 0;       \
+        case O_MAX: O_LOOP(ctype, O_MAXF); return 0;       \
+        case O_SUM: O_LOOP(ctype, O_SUMF); return 0;       \
+        case O_PROD: O_LOOP(ctype, O_PRODF); return 0;     \
+        default: return -2;                                \
+    }
+#define O_CASE_CPLX(ctype)                                 \
+    switch (op) {                                          \
+        case O_SUM: O_LOOP(ctype, O_SUMF); return 0;       \
+        case O_PROD: O_LOOP(ctype, O_PRODF); return 0;     \
+        default: return -2;                                \
+    }
+#define O_CASE_INT(ctype)                                  \
+    switch (op) {                                          \
+        case O_MIN: O_LOOP(ctype, O_MINF); return 0;       \
+        case O_MAX: O_LOOP(ctype, O_MAXF); return 0;       \
+        case O_SUM: O_LOOP(ctype, O_SUMF); return 0;       \
+        case O_PROD: O_LOOP(ctype, O_PRODF); return 0;     \
+        case O_BAND: O_LOOP(ctype, O_ANDF); return 0;      \
+        case O_BOR: O_LOOP(ctype, O_ORF); return 0;        \
+        case O_BXOR: O_LOOP(ctype, O_XORF); return 0;      \
+        default: return -2;                                \
+    }
+
+/* Returns 0, -1 for an invalid datatype (RAISE_ERROR_MSG "invalid data type"),
+ * -2 for an op the datatype's class does not support (RAISE_ERROR_STR
+ * "unsupported reduction on ..."). `count` is int, as in the reference. */
+int oracle_reduce_local(int op, int dt, int count, const void *in, void *inout)
+{
+    switch (dt) {
+        case D_CHAR: O_CASE_FP(char);
+        case D_SCHAR: O_CASE_FP(signed char);
+        case D_SHORT: O_CASE_INT(short);
+        case D_INT: O_CASE_INT(int);
+        case D_LONG: O_CASE_INT(long);
+        case D_LONG_LONG: O_CASE_INT(long long);
+        case D_PTRDIFF_T: O_CASE_FP(ptrdiff_t);
+        case D_UCHAR: O_CASE_INT(unsigned char);
+        case D_USHORT: O_CASE_INT(unsigned short);
+        case D_UINT: O_CASE_INT(unsigned int);
+        case D_ULONG: O_CASE_INT(unsigned long);
+        case D_ULONG_LONG: O_CASE_INT(unsigned long long);
+        case D_INT8: O_CASE_INT(int8_t);
+        case D_INT16: O_CASE_INT(int16_t);
+        case D_INT32: O_CASE_INT(int32_t);
+        case D_INT64: O_CASE_INT(int64_t);
+        case D_UINT8: O_CASE_INT(uint8_t);
+        case D_UINT16: O_CASE_INT(uint16_t);
+        case D_UINT32: O_CASE_INT(uint32_t);
+        case D_UINT64: O_CASE_INT(uint64_t);
+        case D_SIZE_T: O_CASE_INT(size_t);
+        case D_FLOAT: O_CASE_FP(float);
+        case D_DOUBLE: O_CASE_FP(double);
+        case D_LONG_DOUBLE: O_CASE_FP(long double);
+        case D_FLOAT_COMPLEX: O_CASE_CPLX(float _Complex);
+        case D_DOUBLE_COMPLEX: O_CASE_CPLX(double _Complex);
+        default: return -1;
+    }
+}
+
+/* sizeof the C type behind each datatype on x86-64 (0 = not reducible). */
+size_t oracle_type_size(int dt)
+{
+    static const size_t sz[D_COUNT] = {
+        0, 1, 1, 2, 4, 8, 8, 0, 1, 2, 4, 8, 8, 1, 2, 4, 8, 8, 1, 2, 4, 8, 8, 4, 8,
+        sizeof(long double), 8, 16 };
+    return (dt >= 0 && dt < D_COUNT) ? sz[dt] : 0;
+}
+
+/* ------------------------------------------------------------------------------
+ * Ring all-reduce, src/collectives.c:647-764, with P PEs simulated in order.
+ * src[p] / dst[p] are PE p's source and target buffers (dst[p] == src[p] means an
+ * in-place call, handled by the tmp copy of :672-683).  The simulation runs each
+ * step's puts for every PE, then each PE's combine: the pSync waits of :717-722 make
+ * every PE's step-i combine depend only on the step-i put from its left neighbour.
+ * ------------------------------------------------------------------------------ */
+static void ring_chunk(size_t count, int P, size_t c, size_t ts, size_t *n, size_t *disp)
+{
+    /* chunk math, src/collectives.c:697-709 */
+    size_t extra = c < count % (size_t) P;
+    size_t cnt = count / (size_t) P + extra;
+    *n = cnt;
+    *disp = extra ? c * cnt * ts : (c * cnt + count % (size_t) P) * ts;
+}
+
+int oracle_ring(int P, size_t count, int op, int dt, void **src, void **dst)
+{
+    size_t ts = oracle_type_size(dt);
+    if (!ts) return -1;
+    if (count == 0) return 0;
+    if (P == 1) {   /* :664-668 */
+        if (dst[0] != src[0]) memcpy(dst[0], src[0], count * ts);
+        return 0;
+    }
+    void **s = malloc(sizeof(void *) * P);
+    int *tmp = calloc(P, sizeof(int));
+    for (int p = 0; p < P; p++) {
+        s[p] = src[p];
+        if (dst[p] == src[p]) {  /* :672-683 */
+            s[p] = malloc(count * ts);
+            memcpy(s[p], dst[p], count * ts);
+            tmp[p] = 1;
+        }
+    }
+    int rc = 0;
+    /* reduce-scatter, :693-727 */
+    for (int i = 0; i < P - 1; i++) {
+        for (int r = 0; r < P; r++) {
+            int peer = (r + 1) % P;
+            size_t chunk_out = (size_t) ((r - i + P) % P), n, disp;
+            ring_chunk(count, P, chunk_out, ts, &n, &disp);
+            memcpy((uint8_t *) dst[peer] + disp,
+                   i == 0 ? (uint8_t *) s[r] + disp : (uint8_t *) dst[r] + disp, n * ts);
+        }
+        for (int r = 0; r < P; r++) {
+            size_t chunk_in = (size_t) ((r - i - 1 + P) % P), n, disp;
+            ring_chunk(count, P, chunk_in, ts, &n, &disp);
+            rc |= oracle_reduce_local(op, dt, (int) n, (uint8_t *) s[r] + disp,
+                                      (uint8_t *) dst[r] + disp);
+        }
+    }
+    /* all-gather, :737-756 */
+    for (int i = 0; i < P - 1; i++) {
+        for (int r = 0; r < P; r++) {
+            int peer = (r + 1) % P;
+            size_t chunk_out = (size_t) ((r + 1 - i + P) % P), n, disp;
+            ring_chunk(count, P, chunk_out, ts, &n, &disp);
+            memcpy((uint8_t *) dst[peer] + disp, (uint8_t *) dst[r] + disp, n * ts);
+        }
+    }
+    for (int p = 0; p < P; p++) if (tmp[p]) free(s[p]);
+    free(s);
+    free(tmp);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------
+ * Recursive doubling all-reduce, src/collectives.c:850-984, P PEs simulated.
+ * Each PE works on a private copy (current_target, :860/:888) and receives the
+ * peer's full vector into its target (:936-959), then
+ * reduce_local(in = target, inout = current_target) (:961-962): own value is the
+ * left operand.  Non-power-of-two P: PEs >= pow2 fold into PE (id - pow2) first
+ * (:905-926) and receive the final vector from it at the end (:966-975).
+ * ------------------------------------------------------------------------------ */
+int oracle_recdbl(int P, size_t count, int op, int dt, void **src, void **dst)
+{
+    size_t ts = oracle_type_size(dt), bytes;
+    if (!ts) return -1;
+    bytes = count * ts;
+    if (P == 1) {
+        if (dst[0] != src[0]) memcpy(dst[0], src[0], bytes);
+        return 0;
+    }
+    if (count == 0) return 0;
+    int pow2 = 2, log2p = 1, i = P >> 1;
+    while (i != 1) { i >>= 1; pow2 <<= 1; log2p++; }   /* :878-882 */
+    /* The loop above yields pow2 = largest power of two <= P for P >= 2. */
+    void **cur = malloc(sizeof(void *) * P);
+    for (int p = 0; p < P; p++) { cur[p] = malloc(bytes); memcpy(cur[p], src[p], bytes); }
+    int rc = 0;
+    /* extra-peer fold, :905-926 */
+    for (int p = pow2; p < P; p++) {
+        int partner = p - pow2;
+        memcpy(dst[partner], cur[p], bytes);
+        rc |= oracle_reduce_local(op, dt, (int) count, dst[partner], cur[partner]);
+    }
+    /* pairwise exchange, :932-963 */
+    for (int s = 0; s < log2p; s++) {
+        for (int r = 0; r < pow2; r++) memcpy(dst[r ^ (1 << s)], cur[r], bytes);
+        for (int r = 0; r < pow2; r++)
+            rc |= oracle_reduce_local(op, dt, (int) count, dst[r], cur[r]);
+    }
+    /* final result to the extra peers, :966-975; memcpy(target, current), :977 */
+    for (int p = pow2; p < P; p++) memcpy(dst[p], cur[p - pow2], bytes);
+    for (int r = 0; r < pow2; r++) memcpy(dst[r], cur[r], bytes);
+    for (int p = 0; p < P; p++) free(cur[p]);
+    free(cur);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------
+ * Timing helpers for bench.py's cpu_baseline (single core, CLOCK_MONOTONIC as
+ * shmem_internal_wtime, src/shmem_internal.h:549-565).
+ * ------------------------------------------------------------------------------ */
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
+
+/* Runs reduce_local `reps` times over (in, inout) and returns total seconds. */
+double oracle_time_reduce_local(int op, int dt, int count, const void *in, void *inout, int reps)
+{
+    double t0 = now_s();
+    for (int r = 0; r < reps; r++) oracle_reduce_local(op, dt, count, in, inout);
+    return now_s() - t0;
+}
+
+/* ------------------------------------------------------------------------------
+ * Synthetic inputs: splitmix64 of (seed, pe, i), the CPU twin of
+ * sosx_fill (sos_amd/csrc/kernels.hip).  Values are built from bits or by exact
+ * dyadic arithmetic so both sides agree bit for bit.
+ * dist 0: fp uniform [-1,1), ints full-range; dist 1: fp [0.5,2) (complex parts
+ * +-[0.5,1)), ints [-3,3].
+ * ------------------------------------------------------------------------------ */
+static uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static float f32_of(uint64_t h, int dist, int cplx)
+{
+    if (dist == 1) {
+        uint32_t bits = cplx ? (((uint32_t) (h >> 63) << 31) | (126u << 23) | (uint32_t) (h & 0x7FFFFFu))
+                             : (((126u + (uint32_t) (h >> 63)) << 23) | (uint32_t) (h & 0x7FFFFFu));
+        float f;
+        memcpy(&f, &bits, 4);
+        return f;
+    }
+    return (float) (uint32_t) (h >> 40) * 0x1p-23f - 1.0f;
+}
+
+static double f64_of(uint64_t h, int dist, int cplx)
+{
+    if (dist == 1) {
+        uint64_t bits = cplx ? (((h >> 63) << 63) | (1022ull << 52) | (h & 0xFFFFFFFFFFFFFull))
+                             : (((1022ull + (h >> 63)) << 52) | (h & 0xFFFFFFFFFFFFFull));
+        double d;
+        memcpy(&d, &bits, 8);
+        return d;
+    }
+    return (double) (h >> 11) * 0x1p-52 - 1.0;
+}
+
+int oracle_fill(int dt, int dist, uint64_t seed, int pe, void *dst, size_t count, size_t index0)
+{
+    size_t ts = oracle_type_size(dt);
+    if (!ts || dt == D_LONG_DOUBLE) return -1;
+    const uint64_t key = mix64(seed ^ ((uint64_t) (uint32_t) pe << 40));
+    for (size_t j = 0; j < count; j++) {
+        uint64_t i = index0 + j;
+        switch (dt) {
+            case D_FLOAT: ((float *) dst)[j] = f32_of(mix64(key ^ i), dist, 0); break;
+            case D_DOUBLE: ((double *) dst)[j] = f64_of(mix64(key ^ i), dist, 0); break;
+            case D_FLOAT_COMPLEX:
+                ((float *) dst)[2 * j] = f32_of(mix64(key ^ (2 * i)), dist, 1);
+                ((float *) dst)[2 * j + 1] = f32_of(mix64(key ^ (2 * i + 1)), dist, 1);
+                break;
+            case D_DOUBLE_COMPLEX:
+                ((double *) dst)[2 * j] = f64_of(mix64(key ^ (2 * i)), dist, 1);
+                ((double *) dst)[2 * j + 1] = f64_of(mix64(key ^ (2 * i + 1)), dist, 1);
+                break;
+            default: {
+                uint64_t h = mix64(key ^ i);
+                uint64_t v = dist == 1 ? (uint64_t) ((int64_t) (h % 7u) - 3) : h;
+                memcpy((uint8_t *) dst + j * ts, &v, ts);  /* little-endian low bytes */
+            }
+        }
+    }
+    return 0;
+}

@@ -1,0 +1,136 @@
+"""ctypes binding of libsos_amd.so (the MI355X SOS reduction library).
+
+The product path is native: C/C++/HIP in ``sos_amd/csrc`` compiled into
+``sos_amd/libsos_amd.so``.  This module only declares the C ABI (include/sosx.h,
+include/shmem.h, include/shmemx.h) for Python callers.  There is no Python or CPU
+fallback: if the library is missing, :func:`lib` raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsos_amd.so")
+
+# shm_internal_op_t (src/transport_none.h:25-33)
+OPS = {"and": 0, "or": 1, "xor": 2, "min": 3, "max": 4, "sum": 5, "prod": 6}
+
+# shm_internal_datatype_t (src/transport.h:19-49)
+DTYPES = {
+    "signed_byte": 0, "char": 1, "schar": 2, "short": 3, "int": 4, "long": 5,
+    "longlong": 6, "fortran_integer": 7, "int8": 8, "int16": 9, "int32": 10,
+    "int64": 11, "ptrdiff": 12, "uchar": 13, "ushort": 14, "uint": 15, "ulong": 16,
+    "ulonglong": 17, "uint8": 18, "uint16": 19, "uint32": 20, "uint64": 21,
+    "size": 22, "float": 23, "double": 24, "longdouble": 25, "complexf": 26,
+    "complexd": 27,
+}
+
+ORDER_LINEAR, ORDER_TREE = 0, 1
+ALGS = {"auto": 0, "recdbl": 1, "ring": 2, "rechalving": 3, "recdbl_direct": 4}
+DIST_UNIFORM, DIST_PROD = 0, 1
+
+ERRORS = {
+    -1: "invalid data type",
+    -2: "unsupported reduction for this data type",
+    -3: "invalid argument",
+    -4: "HIP runtime error",
+    -5: "RCCL error",
+    -6: "not supported on the device path",
+    -7: "library state error",
+}
+
+
+class SosError(RuntimeError):
+    """A non-zero status from the C ABI."""
+
+    def __init__(self, rc, what):
+        super().__init__(f"{what}: {ERRORS.get(rc, 'error')} (status {rc})")
+        self.rc = rc
+
+
+_LIB = None
+
+_c = ctypes
+_SIGS = {
+    "sosx_dtype_size": (_c.c_size_t, [_c.c_int]),
+    "sosx_check_op": (_c.c_int, [_c.c_int, _c.c_int]),
+    "sosx_combine": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    "sosx_combine3": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                 _c.c_size_t, _c.c_void_p]),
+    "sosx_fold": (_c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
+                             _c.POINTER(_c.c_void_p), _c.c_int, _c.c_size_t, _c.c_void_p]),
+    "sosx_fill": (_c.c_int, [_c.c_int, _c.c_int, _c.c_uint64, _c.c_int, _c.c_void_p,
+                             _c.c_size_t, _c.c_size_t, _c.c_void_p]),
+    "sosx_count_mismatch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_size_t,
+                                       _c.POINTER(_c.c_ulonglong), _c.c_void_p]),
+    "sosx_set_combine_variant": (_c.c_int, [_c.c_int]),
+    "sosx_num_combine_variants": (_c.c_int, []),
+    "sosx_combine_variant_name": (_c.c_char_p, [_c.c_int]),
+    "sosx_build_info": (_c.c_char_p, []),
+}
+
+
+def lib():
+    """Load libsos_amd.so (once) and declare its C signatures."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback for the SOS reduction path)")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        raise SosError(rc, what)
+    return rc
+
+
+def dtype_id(name_or_id):
+    return DTYPES[name_or_id] if isinstance(name_or_id, str) else int(name_or_id)
+
+
+def op_id(name_or_id):
+    return OPS[name_or_id] if isinstance(name_or_id, str) else int(name_or_id)
+
+
+def combine(op, dtype, inout_ptr, in_ptr, count, stream=None):
+    """inout = inout OP in on device memory (sosx_combine)."""
+    return check(lib().sosx_combine(op_id(op), dtype_id(dtype), inout_ptr, in_ptr, count, stream),
+                 "sosx_combine")
+
+
+def combine3(op, dtype, out_ptr, a_ptr, b_ptr, count, stream=None):
+    return check(lib().sosx_combine3(op_id(op), dtype_id(dtype), out_ptr, a_ptr, b_ptr, count,
+                                     stream), "sosx_combine3")
+
+
+def fold(op, dtype, order, out_ptr, in_ptrs, count, stream=None):
+    arr = (ctypes.c_void_p * len(in_ptrs))(*in_ptrs)
+    return check(lib().sosx_fold(op_id(op), dtype_id(dtype), order, out_ptr, arr, len(in_ptrs),
+                                 count, stream), "sosx_fold")
+
+
+def fill(dtype, dist, seed, pe, dst_ptr, count, index0=0, stream=None):
+    return check(lib().sosx_fill(dtype_id(dtype), dist, seed, pe, dst_ptr, count, index0, stream),
+                 "sosx_fill")
+
+
+def count_mismatch(a_ptr, b_ptr, count, elem_size, stream=None):
+    out = ctypes.c_ulonglong(0)
+    check(lib().sosx_count_mismatch(a_ptr, b_ptr, count, elem_size, ctypes.byref(out), stream),
+          "sosx_count_mismatch")
+    return out.value
+
+
+def dtype_size(dtype):
+    return lib().sosx_dtype_size(dtype_id(dtype))

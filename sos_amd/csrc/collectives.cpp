@@ -1,0 +1,392 @@
+// collectives.cpp -- the SOS team reduction on MI355X: argument checks, algorithm
+// dispatch, and the executors that run a per-PE plan (plan.h).
+//
+// shmem_internal_op_to_all (src/shmem_collectives.h:169-239) picks linear/tree
+// (NIC atomics), recdbl_sw or ring.  Here there are no NIC atomics, so AUTO is SOS's
+// non-atomic branch: recdbl below SHMEM_COLL_SIZE_CROSSOVER bytes, ring above; the
+// GPU ring is bit-exact with SOS's (same chunks, same fold order) but moves bytes by a
+// direct exchange over all xGMI links at once.
+//
+// Executors:
+//   * RCCL: each round's transfers are ncclSend/ncclRecv (byte views) inside one
+//     ncclGroupStart/End on the PE's stream, followed by the round's fused folds
+//     (sosx_fold) on the same stream -- no host round trip until the call returns.
+//   * loopback (sosx_loopback_allreduce): P PEs' buffers on one GPU, transfers as
+//     device-to-device copies matched in the same FIFO-per-peer order RCCL uses.
+// Host-resident source/target are staged through device memory (H2D, device
+// reduction, D2H), as the north star's host-symmetric-heap path.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <deque>
+#include <map>
+#include <tuple>
+#include <vector>
+
+#include "api_internal.h"
+#include "dtypes.h"
+#include "plan.h"
+#include "runtime.h"
+#include "shmemx.h"
+#include "sosx.h"
+
+using namespace sosrt;
+using sosplan::Plan;
+
+namespace {
+
+// ---------------------------------------------------------------------------------
+// optional per-phase timing (sosx_prof_*), HIP events on the PE stream
+// ---------------------------------------------------------------------------------
+struct Prof {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> fold_ev, xfer_ev;
+    size_t nf = 0, nx = 0;
+    double fold_ms = 0, xfer_ms = 0, call_ms = 0;
+    long nfold = 0, nxfer = 0, ncall = 0;
+    hipEvent_t get(std::vector<std::pair<hipEvent_t, hipEvent_t>> &v, size_t &n, bool second)
+    {
+        if (!second) {
+            if (n == v.size()) {
+                hipEvent_t a, b;
+                (void)hipEventCreate(&a);
+                (void)hipEventCreate(&b);
+                v.push_back({a, b});
+            }
+            return v[n].first;
+        }
+        return v[n++].second;
+    }
+    void collect()
+    {
+        for (size_t i = 0; i < nf; ++i) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, fold_ev[i].first, fold_ev[i].second) == hipSuccess) fold_ms += ms;
+        }
+        for (size_t i = 0; i < nx; ++i) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, xfer_ev[i].first, xfer_ev[i].second) == hipSuccess) xfer_ms += ms;
+        }
+        nfold += (long)nf;
+        nxfer += (long)nx;
+        nf = nx = 0;
+    }
+};
+Prof g_prof;
+
+struct Bufs {
+    const char *src;
+    char *dst;
+    char *scr;
+    const char *at(int b, uint64_t off) const
+    {
+        return (b == sosplan::SRC ? src : b == sosplan::DST ? (const char *)dst : (const char *)scr) + off;
+    }
+    char *wat(int b, uint64_t off) const { return (char *)at(b, off); }
+};
+
+// Run one round's local operations.
+int run_locals(const sosplan::Round &r, const Bufs &b, int op, int dt, hipStream_t stream)
+{
+    for (const auto &l : r.ops) {
+        if (l.kind == sosplan::COPY) {
+            if (b.at(l.in_buf[0], l.in_off[0]) == b.at(l.out_buf, l.out_off)) continue;
+            hipError_t e = hipMemcpyAsync(b.wat(l.out_buf, l.out_off), b.at(l.in_buf[0], l.in_off[0]),
+                                          l.count, hipMemcpyDefault, stream);
+            if (e != hipSuccess) return SOSX_ERR_HIP;
+            continue;
+        }
+        const void *ins[SOSX_MAX_FOLD];
+        for (int k = 0; k < l.nin; ++k) ins[k] = b.at(l.in_buf[k], l.in_off[k]);
+        if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.fold_ev, g_prof.nf, false), stream);
+        int rc = sosx_fold(op, dt, l.order, b.wat(l.out_buf, l.out_off), ins, l.nin, l.count, stream);
+        if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.fold_ev, g_prof.nf, true), stream);
+        if (rc) return rc;
+    }
+    return SOSX_OK;
+}
+
+// RCCL executor: one ncclGroup per round, folds after it, all on `stream`.
+int exec_rccl(const Plan &p, const Team &t, const Bufs &b, int op, int dt, hipStream_t stream)
+{
+    State &s = st();
+    for (const auto &r : p.rounds) {
+        if (!r.xfers.empty()) {
+            if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, false), stream);
+            if (ncclGroupStart() != ncclSuccess) return SOSX_ERR_RCCL;
+            for (const auto &x : r.xfers) {
+                const int peer = t.world_rank(x.peer);
+                ncclResult_t rc = x.send
+                    ? ncclSend(b.at(x.buf, x.off), x.bytes, ncclUint8, peer, s.comm, stream)
+                    : ncclRecv(b.wat(x.buf, x.off), x.bytes, ncclUint8, peer, s.comm, stream);
+                if (rc != ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    return SOSX_ERR_RCCL;
+                }
+            }
+            if (ncclGroupEnd() != ncclSuccess) return SOSX_ERR_RCCL;
+            if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, true), stream);
+        }
+        int rc = run_locals(r, b, op, dt, stream);
+        if (rc) return rc;
+    }
+    return SOSX_OK;
+}
+
+// Plan cache: the same call shape every step reuses its plan.
+const Plan &cached_plan(int alg, int P, int me, uint64_t count, uint64_t ts, unsigned smis,
+                        unsigned dmis)
+{
+    static std::map<std::tuple<int, int, int, uint64_t, uint64_t, unsigned, unsigned>, Plan> cache;
+    auto key = std::make_tuple(alg, P, me, count, ts, smis, dmis);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    if (cache.size() > 64) cache.clear();
+    Plan p;
+    if (sosplan::build(alg, P, me, count, ts, smis, dmis, &p) != SOSX_OK)
+        raise_error("internal: cannot build reduction plan (alg %d, P %d)", alg, P);
+    return cache.emplace(key, std::move(p)).first->second;
+}
+
+const char *status_text(int rc)
+{
+    switch (rc) {
+        case SOSX_ERR_DTYPE: return "invalid data type";
+        case SOSX_ERR_OP: return "unsupported reduction for this data type";
+        case SOSX_ERR_UNSUPPORTED: return "long double reductions are not supported on the gfx950 device path";
+        case SOSX_ERR_HIP: return "HIP runtime failure";
+        case SOSX_ERR_RCCL: return "RCCL failure";
+        default: return "invalid argument";
+    }
+}
+
+// shmem_internal_op_to_all for this PE over team t.
+void op_to_all(void *target, const void *source, size_t count, size_t ts, const Team &t, int op,
+               int dt, const char *fn)
+{
+    State &s = st();
+    if (count == 0) return;
+    const size_t bytes = count * ts;
+    if (t.size == 1) {
+        // PE_size 1: copy (src/collectives.c:664-668), no combine, any datatype
+        if (target != source)
+            hip_check(hipMemcpyAsync(target, source, bytes, hipMemcpyDefault, s.stream), fn);
+        hip_check(hipStreamSynchronize(s.stream), fn);
+        return;
+    }
+    int rc = sos_check_op(op, dt);
+    if (rc == SOSX_OK && sos_dtype_info(dt).kind == K_LDBL) rc = SOSX_ERR_UNSUPPORTED;
+    if (rc) raise_error("%s: %s (datatype %d, op %d)", fn, status_text(rc), dt, op);
+
+    int alg = sosplan::resolve_alg(s.reduce_alg, bytes, s.coll_size_crossover);
+    if ((alg == SOSX_ALG_RING || alg == SOSX_ALG_RECDBL_DIRECT) && t.size > SOSX_MAX_FOLD)
+        alg = SOSX_ALG_RECHALVING;
+
+    // residency: device pointers run in place; host memory is staged through HBM
+    const bool dev_src = is_device_ptr(source);
+    const bool dev_dst = target == source ? dev_src : is_device_ptr(target);
+    const char *dsrc = (const char *)source;
+    char *ddst = (char *)target;
+    if (!dev_src || !dev_dst) {
+        const size_t half = (bytes + 255) / 256 * 256;
+        char *stg = (char *)stage(2 * half);
+        if (!dev_src) {
+            hip_check(hipMemcpyAsync(stg, source, bytes, hipMemcpyHostToDevice, s.stream), "H2D");
+            dsrc = stg;
+        }
+        if (!dev_dst) ddst = target == source ? stg : stg + half;
+    }
+    const Plan &p = cached_plan(alg, t.size, t.my_idx, count, ts, (unsigned)((uintptr_t)dsrc & 15),
+                                (unsigned)((uintptr_t)ddst & 15));
+    Bufs b{dsrc, ddst, p.scratch_bytes ? (char *)scratch(p.scratch_bytes) : nullptr};
+    if (g_prof.on) g_prof.ncall++;
+    rc = exec_rccl(p, t, b, op, dt, s.stream);
+    if (rc) raise_error("%s: %s", fn, status_text(rc));
+    if (!dev_dst)
+        hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
+    hip_check(hipStreamSynchronize(s.stream), fn);
+    if (g_prof.on) g_prof.collect();
+}
+
+// SHMEM_ERR_CHECK_OVERLAP (src/shmem_internal.h:319-336), complete overlap allowed
+void check_overlap(const void *a, const void *b, size_t bytes, const char *fn)
+{
+    if (a == b || bytes == 0) return;
+    const char *lo = (const char *)(a < b ? a : b), *hi = (const char *)(a < b ? b : a);
+    if (lo + bytes > hi)
+        raise_error("%s: Argument \"dest\" [%p..%p) overlaps argument (%p)", fn, (const void *)lo,
+                    (const void *)(lo + bytes), (const void *)hi);
+}
+
+void check_symmetric(const void *p, size_t bytes, const char *what, const char *fn)
+{
+    if (st().error_checking && bytes && !is_symmetric(p, bytes))
+        raise_error("%s: argument \"%s\" (%p, %zu bytes) is not symmetric", fn, what, p, bytes);
+}
+
+}  // namespace
+
+extern "C" {
+
+void sos_api_to_all(void *target, const void *source, int nreduce, size_t type_size,
+                    int PE_start, int logPE_stride, int PE_size, void *pWrk, long *pSync, int op,
+                    int datatype, const char *fn)
+{
+    check_initialized(fn);
+    State &s = st();
+    const int stride = 1 << logPE_stride;
+    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) > s.n_pes)
+        raise_error("%s: Invalid active set (PE_start = %d, PE_stride = %d, PE_size = %d)", fn,
+                    PE_start, stride, PE_size);
+    if (!(s.my_pe >= PE_start && s.my_pe <= PE_start + ((PE_size - 1) * stride) &&
+          (s.my_pe - PE_start) % stride == 0))
+        raise_error("%s: Calling PE (%d) is not a member of the active set", fn, s.my_pe);
+    if (nreduce < 0)
+        raise_error("%s: Argument nreduce must be greater or equal to zero (%ld)", fn, (long)nreduce);
+    const size_t bytes = (size_t)nreduce * type_size;
+    check_symmetric(target, bytes, "target", fn);
+    check_symmetric(source, bytes, "source", fn);
+    const size_t wrk = (size_t)(nreduce / 2 + 1 > SHMEM_REDUCE_MIN_WRKDATA_SIZE
+                                    ? nreduce / 2 + 1 : SHMEM_REDUCE_MIN_WRKDATA_SIZE);
+    check_symmetric(pWrk, type_size * wrk, "pWrk", fn);
+    check_symmetric(pSync, sizeof(long) * SHMEM_REDUCE_SYNC_SIZE, "pSync", fn);
+    check_overlap(target, source, bytes, fn);
+    // pWrk is never touched by any SOS reduction algorithm; pSync holds
+    // SHMEM_SYNC_VALUE on entry and is left so (RCCL does the synchronisation).
+    Team t;
+    t.start = PE_start;
+    t.stride = stride;
+    t.size = PE_size;
+    t.my_idx = (s.my_pe - PE_start) / stride;
+    t.valid = true;
+    op_to_all(target, source, (size_t)nreduce, type_size, t, op, datatype, fn);
+}
+
+int sos_api_reduce(shmem_team_t team, void *dest, const void *source, size_t nreduce,
+                   size_t type_size, int op, int datatype, const char *fn)
+{
+    check_initialized(fn);
+    Team *t = team_from_handle(team);
+    if (!t || !t->valid) raise_error("%s: invalid team", fn);
+    const size_t bytes = nreduce * type_size;
+    check_symmetric(dest, bytes, "dest", fn);
+    check_symmetric(source, bytes, "source", fn);
+    check_overlap(dest, source, bytes, fn);
+    if (t->my_idx < 0) raise_error("%s: calling PE is not a member of the team", fn);
+    op_to_all(dest, source, nreduce, type_size, *t, op, datatype, fn);
+    return 0;
+}
+
+int shmemx_reduce_local(int op, int datatype, size_t count, const void *in, void *inout)
+{
+    check_initialized("shmemx_reduce_local");
+    return sosx_combine(op, datatype, inout, in, count, st().stream);
+}
+
+// ---- phase timing -----------------------------------------------------------------
+void sosx_prof_enable(int on)
+{
+    g_prof.on = on != 0;
+    g_prof.fold_ms = g_prof.xfer_ms = 0;
+    g_prof.nfold = g_prof.nxfer = g_prof.ncall = 0;
+}
+
+void sosx_prof_get(double *fold_ms, double *xfer_ms, long *nfold, long *nxfer, long *ncall)
+{
+    if (fold_ms) *fold_ms = g_prof.fold_ms;
+    if (xfer_ms) *xfer_ms = g_prof.xfer_ms;
+    if (nfold) *nfold = g_prof.nfold;
+    if (nxfer) *nxfer = g_prof.nxfer;
+    if (ncall) *ncall = g_prof.ncall;
+}
+
+// ---- single-GPU loopback team -------------------------------------------------------
+int sosx_loopback_allreduce(int alg, int P, int op, int datatype, void *const *srcs,
+                            void *const *dsts, size_t count, void *stream)
+{
+    if (P < 1 || P > SOSX_MAX_FOLD || !srcs || !dsts) return SOSX_ERR_ARG;
+    int rc = sos_check_op(op, datatype);
+    if (rc) return rc;
+    if (sos_dtype_info(datatype).kind == K_LDBL && P > 1) return SOSX_ERR_UNSUPPORTED;
+    const size_t ts = sos_dtype_info(datatype).size;
+    hipStream_t sm = (hipStream_t)stream;
+    const int a = sosplan::resolve_alg(alg, count * ts, 16384);
+    std::vector<Plan> plans(P);
+    std::vector<void *> scr(P, nullptr);
+    for (int p = 0; p < P; ++p) {
+        rc = sosplan::build(a, P, p, count, ts, (unsigned)((uintptr_t)srcs[p] & 15),
+                            (unsigned)((uintptr_t)dsts[p] & 15), &plans[p]);
+        if (rc) return rc;
+        if (plans[p].scratch_bytes && hipMalloc(&scr[p], plans[p].scratch_bytes) != hipSuccess)
+            return SOSX_ERR_HIP;
+    }
+    struct Send { const char *ptr; uint64_t bytes; int from; };
+    std::map<std::pair<int, int>, std::deque<Send>> q;  // (from, to) FIFO, as RCCL matches
+    std::vector<size_t> k(P, 0);
+    std::vector<int> posted(P, 0), outstanding(P, 0);
+    std::vector<std::vector<char>> recv_done(P);
+    auto bufs = [&](int p) { return Bufs{(const char *)srcs[p], (char *)dsts[p], (char *)scr[p]}; };
+    for (;;) {
+        bool progress = false, all_done = true;
+        for (int p = 0; p < P; ++p) {
+            if (k[p] >= plans[p].rounds.size()) continue;
+            all_done = false;
+            const auto &r = plans[p].rounds[k[p]];
+            const Bufs b = bufs(p);
+            if (!posted[p]) {
+                for (const auto &x : r.xfers)
+                    if (x.send) {
+                        q[{p, x.peer}].push_back(Send{b.at(x.buf, x.off), x.bytes, p});
+                        outstanding[p]++;
+                    }
+                recv_done[p].assign(r.xfers.size(), 0);
+                posted[p] = 1;
+                progress = true;
+            }
+            bool recvs_ok = true;
+            for (size_t i = 0; i < r.xfers.size(); ++i) {
+                const auto &x = r.xfers[i];
+                if (x.send || recv_done[p][i]) continue;
+                auto &fifo = q[{x.peer, p}];
+                // FIFO per (peer, me): only the oldest pending send from that peer matches
+                bool earlier_pending = false;
+                for (size_t j = 0; j < i; ++j)
+                    if (!r.xfers[j].send && r.xfers[j].peer == x.peer && !recv_done[p][j]) earlier_pending = true;
+                if (earlier_pending || fifo.empty()) {
+                    recvs_ok = false;
+                    continue;
+                }
+                Send snd = fifo.front();
+                fifo.pop_front();
+                if (snd.bytes != x.bytes) {
+                    for (auto v : scr) if (v) (void)hipFree(v);
+                    return SOSX_ERR_ARG;  // plan mismatch between PEs
+                }
+                if (hipMemcpyAsync(b.wat(x.buf, x.off), snd.ptr, x.bytes, hipMemcpyDeviceToDevice, sm) != hipSuccess)
+                    return SOSX_ERR_HIP;
+                outstanding[snd.from]--;
+                recv_done[p][i] = 1;
+                progress = true;
+            }
+            if (recvs_ok && outstanding[p] == 0) {
+                rc = run_locals(r, b, op, datatype, sm);
+                if (rc) return rc;
+                k[p]++;
+                posted[p] = 0;
+                progress = true;
+            }
+        }
+        if (all_done) break;
+        if (!progress) {
+            for (auto v : scr) if (v) (void)hipFree(v);
+            return SOSX_ERR_ARG;  // deadlock: inconsistent plans
+        }
+    }
+    hipError_t e = hipStreamSynchronize(sm);
+    for (auto v : scr)
+        if (v) (void)hipFree(v);
+    return e == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
+}
+
+}  // extern "C"

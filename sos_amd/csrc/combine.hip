@@ -1,0 +1,218 @@
+// combine.hip -- the local combine inout = inout OP in (sosx_combine / sosx_combine3),
+// the device replacement for shmem_internal_reduce_local (src/shmem_internal_op.h:305-339).
+//
+// A 3-stream elementwise pass (read in, read inout, write inout; 1 op per element) is
+// HBM-bandwidth bound.  The kernel is built for the HBM roofline:
+//   * 16-byte (dwordx4) loads/stores per lane, U=4 vectors per lane per operand, all
+//     2U loads of a tile issued before the first combine (8 x 16 B in flight/lane);
+//   * 256-thread workgroups, one 16 KiB-per-operand tile per workgroup, >> 256
+//     workgroups per launch (a 128Mi fp32 combine is 32768 workgroups), the ragged
+//     head/tail handled by one extra workgroup so the hot tiles carry no bounds checks;
+//   * relative 16-B misalignment of the operands falls back to element loads.
+// Tuning variants (bench.py --variants) are compiled for the fp32 sum only.
+#include "elementwise.h"
+
+namespace sos {
+
+// ---------------------------------------------------------------------------------
+// out = a OP b (out may alias a): the local combine.
+// ---------------------------------------------------------------------------------
+template <class T, class OP, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kThreads) void k_combine3(T *__restrict__ out, const T *a,
+                                                         const T *b, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    const u32x4 *A = reinterpret_cast<const u32x4 *>(a + g.head);
+    const u32x4 *B = reinterpret_cast<const u32x4 *>(b + g.head);
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t base = t * (size_t)(kThreads * U) + threadIdx.x;
+        u32x4 ra[U], rb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ra[u] = ldv<NTL>(A + base + u * kThreads);
+            rb[u] = ldv<NTL>(B + base + u * kThreads);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) stv<NTS>(O + base + u * kThreads, apply<T, OP>(ra[u], rb[u]));
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n;
+             i += kThreads)
+            out[i] = OP::f(a[i], b[i]);
+    }
+}
+
+// LDS-staged partner tile: the partner vector `b` is brought into LDS by LDS-DMA
+// (global_load_lds_dwordx4) while `a` streams into registers.  Kept as a measured
+// alternative (bench --variants); for a pure 3-stream combine the LDS round trip
+// buys nothing over register staging (MI355X guide, "glds vs register staging").
+template <class T, class OP, int U>
+__global__ __launch_bounds__(kThreads) void k_combine3_lds(T *__restrict__ out, const T *a,
+                                                             const T *b, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    __shared__ __attribute__((aligned(16))) u32x4 tile[kThreads * U];
+    const u32x4 *A = reinterpret_cast<const u32x4 *>(a + g.head);
+    const u32x4 *B = reinterpret_cast<const u32x4 *>(b + g.head);
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t base = t * (size_t)(kThreads * U) + threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            // LDS destination = wave-uniform base + lane*16 (lane-linear image).
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(B + base + u * kThreads),
+                (__attribute__((address_space(3))) void *)(&tile[u * kThreads + wave * 64]), 16,
+                0, 0);
+        }
+        u32x4 ra[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) ra[u] = A[base + u * kThreads];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            O[base + u * kThreads] = apply<T, OP>(ra[u], tile[u * kThreads + wave * 64 + lane]);
+        __builtin_amdgcn_s_barrier();
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n;
+             i += kThreads)
+            out[i] = OP::f(a[i], b[i]);
+    }
+}
+
+// Relative misalignment between the operands (not 16-B congruent): element loads.
+template <class T, class OP>
+__global__ __launch_bounds__(kThreads) void k_combine3_scalar(T *__restrict__ out, const T *a,
+                                                                const T *b, size_t n)
+{
+    const size_t stride = (size_t)gridDim.x * kThreads;
+    for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
+        out[i] = OP::f(a[i], b[i]);
+}
+
+}  // namespace sos
+
+using namespace sos;
+
+namespace {
+
+int g_variant = 0;
+
+struct VariantDesc {
+    const char *name;
+};
+const VariantDesc kVariants[] = {
+    {"u4_nt"},             // 0: default: U=4, nontemporal loads+stores, one tile/workgroup
+    {"u1_nt"},             // 1
+    {"u2_nt"},             // 2
+    {"u8_nt"},             // 3
+    {"u4_ntload"},         // 4: nontemporal loads, plain stores
+    {"u4_plain"},          // 5: plain loads/stores
+    {"u1_plain"},          // 6
+    {"u4_nt_persist4096"}, // 7: grid-stride over 4096 workgroups
+    {"u2_nt_persist2048"}, // 8
+    {"u4_lds_dma"},        // 9: partner tile via global_load_lds (LDS-DMA)
+};
+constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
+
+template <class T, class OP, int U, bool NTL, bool NTS>
+int launch_combine3_vec(T *out, const T *a, const T *b, size_t n, hipStream_t st, size_t cap)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), U);
+    unsigned grid = grid_for(g, cap);
+    hipLaunchKernelGGL((k_combine3<T, OP, U, NTL, NTS>), dim3(grid), dim3(kThreads), 0, st, out,
+                       a, b, g);
+    return hip_ok(hipGetLastError());
+}
+
+template <class T, class OP>
+int launch_combine3(T *out, const T *a, const T *b, size_t n, hipStream_t st)
+{
+    if (n == 0) return SOSX_OK;
+    const uintptr_t o = (uintptr_t)out, pa = (uintptr_t)a, pb = (uintptr_t)b;
+    const bool congruent = ((o ^ pa) & 15) == 0 && ((o ^ pb) & 15) == 0 && (o % sizeof(T)) == 0;
+    if (!congruent || sizeof(T) > 16) {
+        size_t blocks = (n + kThreads - 1) / kThreads;
+        if (blocks > 8192) blocks = 8192;
+        hipLaunchKernelGGL((k_combine3_scalar<T, OP>), dim3((unsigned)blocks), dim3(kThreads), 0,
+                           st, out, a, b, n);
+        return hip_ok(hipGetLastError());
+    }
+    if constexpr (std::is_same<T, float>::value && std::is_same<OP, OpSum>::value) {
+        switch (g_variant) {
+            case 1: return launch_combine3_vec<T, OP, 1, true, true>(out, a, b, n, st, kNoCap);
+            case 2: return launch_combine3_vec<T, OP, 2, true, true>(out, a, b, n, st, kNoCap);
+            case 3: return launch_combine3_vec<T, OP, 8, true, true>(out, a, b, n, st, kNoCap);
+            case 4: return launch_combine3_vec<T, OP, 4, true, false>(out, a, b, n, st, kNoCap);
+            case 5: return launch_combine3_vec<T, OP, 4, false, false>(out, a, b, n, st, kNoCap);
+            case 6: return launch_combine3_vec<T, OP, 1, false, false>(out, a, b, n, st, kNoCap);
+            case 7: return launch_combine3_vec<T, OP, 4, true, true>(out, a, b, n, st, 4096);
+            case 8: return launch_combine3_vec<T, OP, 2, true, true>(out, a, b, n, st, 2048);
+            case 9: {
+                Geom g = make_geom(o, n, sizeof(T), 4);
+                hipLaunchKernelGGL((k_combine3_lds<T, OP, 4>), dim3(grid_for(g, kNoCap)),
+                                   dim3(kThreads), 0, st, out, a, b, g);
+                return hip_ok(hipGetLastError());
+            }
+            default: break;
+        }
+    }
+    // Default: U=4, nontemporal loads and stores (measured 80.5% vs 70.5% of the 8 TB/s
+    // HBM peak for plain loads/stores on the 128Mi fp32 sum; profiles/r1_*).
+    return launch_combine3_vec<T, OP, 4, true, true>(out, a, b, n, st, kNoCap);
+}
+
+struct Combine3Fn {
+    template <class T, class OP>
+    static int run(void *out, const void *a, const void *b, size_t n, hipStream_t st)
+    {
+        return launch_combine3<T, OP>((T *)out, (const T *)a, (const T *)b, n, st);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+size_t sosx_dtype_size(int dtype) { return sos_dtype_info(dtype).size; }
+
+int sosx_check_op(int op, int dtype) { return sos_check_op(op, dtype); }
+
+int sosx_combine3(int op, int dtype, void *out, const void *a, const void *b, size_t count,
+                  void *stream)
+{
+    if (count == 0) return sos_check_op(op, dtype);
+    if (!out || !a || !b) return SOSX_ERR_ARG;
+    return dispatch<Combine3Fn>(op, dtype, out, a, b, count, as_stream(stream));
+}
+
+int sosx_combine(int op, int dtype, void *inout, const void *in, size_t count, void *stream)
+{
+    return sosx_combine3(op, dtype, inout, inout, in, count, stream);
+}
+
+int sosx_set_combine_variant(int variant)
+{
+    int prev = g_variant;
+    if (variant >= 0 && variant < kNumVariants) g_variant = variant;
+    return prev;
+}
+
+int sosx_num_combine_variants(void) { return kNumVariants; }
+
+const char *sosx_combine_variant_name(int variant)
+{
+    return (variant >= 0 && variant < kNumVariants) ? kVariants[variant].name : "";
+}
+
+const char *sosx_build_info(void)
+{
+    return "sos_amd: gfx950 HIP kernels (combine/fold/fill), hipcc " __clang_version__;
+}
+
+}  // extern "C"

@@ -1,0 +1,331 @@
+// plan.cpp -- the SOS team-reduction schedules as per-PE plans (see plan.h).
+#include "plan.h"
+
+#include <string.h>
+
+namespace sosplan {
+
+namespace {
+
+inline uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+Xfer xf(int send, int peer, int buf, uint64_t off, uint64_t bytes)
+{
+    Xfer x;
+    x.send = send;
+    x.peer = peer;
+    x.buf = buf;
+    x.off = off;
+    x.bytes = bytes;
+    return x;
+}
+
+Local fold2(int out_buf, uint64_t out_off, int a_buf, uint64_t a_off, int b_buf, uint64_t b_off,
+            uint64_t count)
+{
+    Local l;
+    memset(&l, 0, sizeof(l));
+    l.kind = FOLD;
+    l.order = SOSX_ORDER_LINEAR;
+    l.out_buf = out_buf;
+    l.out_off = out_off;
+    l.nin = 2;
+    l.in_buf[0] = a_buf;
+    l.in_off[0] = a_off;
+    l.in_buf[1] = b_buf;
+    l.in_off[1] = b_off;
+    l.count = count;
+    return l;
+}
+
+// Largest power of two <= P (src/collectives.c:878-882 for P >= 2).
+int pow2_floor(int P)
+{
+    int p = 1;
+    while (p * 2 <= P) p *= 2;
+    return p;
+}
+
+// RING and RECDBL_DIRECT share the data movement: a direct reduce-scatter of the SOS
+// ring chunks (chunk c is owned, folded and broadcast by team index c), then a
+// direct allgather.  Only the fold order differs.
+int build_direct(int alg, int P, int me, uint64_t count, uint64_t ts, unsigned src_mis,
+                 unsigned dst_mis, Plan *plan)
+{
+    if (P > SOSX_MAX_FOLD) return SOSX_ERR_ARG;
+    uint64_t n_me, first_me;
+    ring_chunk(count, P, me, &n_me, &first_me);
+    const uint64_t my_bytes = n_me * ts;
+    // Scratch slot for each peer's copy of my chunk, 16-B congruent with my DST chunk.
+    const uint64_t mis = (dst_mis + first_me * ts) & 15;
+    const uint64_t stride = round_up(my_bytes + 16, 256);
+    auto slot = [&](int peer) { return (uint64_t)((peer - me - 1 + P) % P) * stride + mis; };
+    (void)src_mis;
+    plan->scratch_bytes = (uint64_t)(P - 1) * stride;
+
+    Round rs;  // reduce-scatter exchange
+    for (int k = 1; k < P; ++k) {
+        const int peer = (me + k) % P;
+        uint64_t n_p, first_p;
+        ring_chunk(count, P, peer, &n_p, &first_p);
+        if (n_p) rs.xfers.push_back(xf(1, peer, SRC, first_p * ts, n_p * ts));
+        if (n_me) rs.xfers.push_back(xf(0, peer, SCR, slot(peer), my_bytes));
+    }
+    if (n_me) {
+        Local l;
+        memset(&l, 0, sizeof(l));
+        l.kind = FOLD;
+        l.out_buf = DST;
+        l.out_off = first_me * ts;
+        l.nin = P;
+        l.count = n_me;
+        if (alg == SOSX_ALG_RING) {
+            // ring fold of chunk c starts at PE c (= me) and walks right:
+            // ((s_me OP s_me+1) OP ...) OP s_me-1  (src/collectives.c:711-726)
+            l.order = SOSX_ORDER_LINEAR;
+            for (int k = 0; k < P; ++k) {
+                const int pe = (me + k) % P;
+                l.in_buf[k] = pe == me ? SRC : SCR;
+                l.in_off[k] = pe == me ? first_me * ts : slot(pe);
+            }
+        } else {
+            // recdbl_sw tree over team indices 0..P-1
+            l.order = SOSX_ORDER_TREE;
+            for (int pe = 0; pe < P; ++pe) {
+                l.in_buf[pe] = pe == me ? SRC : SCR;
+                l.in_off[pe] = pe == me ? first_me * ts : slot(pe);
+            }
+        }
+        rs.ops.push_back(l);
+    }
+    plan->rounds.push_back(rs);
+
+    Round ag;  // direct allgather of the owned chunks
+    for (int k = 1; k < P; ++k) {
+        const int peer = (me + k) % P;
+        uint64_t n_p, first_p;
+        ring_chunk(count, P, peer, &n_p, &first_p);
+        if (n_me) ag.xfers.push_back(xf(1, peer, DST, first_me * ts, my_bytes));
+        if (n_p) ag.xfers.push_back(xf(0, peer, DST, first_p * ts, n_p * ts));
+    }
+    plan->rounds.push_back(ag);
+    return SOSX_OK;
+}
+
+// recdbl_sw butterfly, step for step (src/collectives.c:850-984).  The current vector
+// lives in DST (the reference keeps it in a malloc'd copy and uses the target as the
+// receive buffer; here the receive buffer is scratch, so no final copy is needed).
+int build_recdbl(int P, int me, uint64_t count, uint64_t ts, unsigned dst_mis, Plan *plan)
+{
+    const int pow2 = pow2_floor(P);
+    const uint64_t bytes = count * ts;
+    const uint64_t soff = dst_mis & 15;  // scratch congruent with DST
+    plan->scratch_bytes = round_up(bytes + 16, 256);
+    if (me >= pow2) {
+        // extra PE: hand the vector to its partner (:905-917), receive the result (:966-975)
+        Round a;
+        a.xfers.push_back(xf(1, me - pow2, SRC, 0, bytes));
+        plan->rounds.push_back(a);
+        Round b;
+        b.xfers.push_back(xf(0, me - pow2, DST, 0, bytes));
+        plan->rounds.push_back(b);
+        return SOSX_OK;
+    }
+    int cur = SRC;
+    if (me < P - pow2) {
+        // fold the extra PE's vector: current = current OP extra (:920-926)
+        Round a;
+        a.xfers.push_back(xf(0, me + pow2, SCR, soff, bytes));
+        a.ops.push_back(fold2(DST, 0, cur, 0, SCR, soff, count));
+        plan->rounds.push_back(a);
+        cur = DST;
+    }
+    for (int d = 1; d < pow2; d <<= 1) {
+        // pairwise exchange at distance d: current = current OP peer (:932-963)
+        Round r;
+        r.xfers.push_back(xf(1, me ^ d, cur, 0, bytes));
+        r.xfers.push_back(xf(0, me ^ d, SCR, soff, bytes));
+        r.ops.push_back(fold2(DST, 0, cur, 0, SCR, soff, count));
+        plan->rounds.push_back(r);
+        cur = DST;
+    }
+    if (me < P - pow2) {
+        Round b;
+        b.xfers.push_back(xf(1, me + pow2, DST, 0, bytes));
+        plan->rounds.push_back(b);
+    }
+    return SOSX_OK;
+}
+
+// Recursive halving (reduce-scatter at distance 1, 2, 4, ...) + recursive doubling
+// (allgather at distance ..., 4, 2, 1), with the recdbl_sw fold of extra PEs.
+int build_rechalving(int P, int me, uint64_t count, uint64_t ts, unsigned dst_mis, Plan *plan)
+{
+    const int pow2 = pow2_floor(P);
+    const uint64_t bytes = count * ts;
+    plan->scratch_bytes = round_up((count - count / 2) * ts + 16, 256);
+    if (me >= pow2) {
+        Round a;
+        a.xfers.push_back(xf(1, me - pow2, SRC, 0, bytes));
+        plan->rounds.push_back(a);
+        Round b;
+        b.xfers.push_back(xf(0, me - pow2, DST, 0, bytes));
+        plan->rounds.push_back(b);
+        return SOSX_OK;
+    }
+    int cur = SRC;
+    if (me < P - pow2) {
+        plan->scratch_bytes = round_up(bytes + 16, 256);
+        const uint64_t soff = dst_mis & 15;
+        Round a;
+        a.xfers.push_back(xf(0, me + pow2, SCR, soff, bytes));
+        a.ops.push_back(fold2(DST, 0, cur, 0, SCR, soff, count));
+        plan->rounds.push_back(a);
+        cur = DST;
+    }
+    struct Seg { uint64_t lo, hi, mid; bool low; };
+    std::vector<Seg> stack;
+    uint64_t lo = 0, hi = count;
+    for (int d = 1; d < pow2; d <<= 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        const bool low = (me & d) == 0;
+        const uint64_t klo = low ? lo : mid, khi = low ? mid : hi;  // kept
+        const uint64_t slo = low ? mid : lo, shi = low ? hi : mid;  // sent
+        const uint64_t soff = (dst_mis + klo * ts) & 15;
+        Round r;
+        if (shi > slo) r.xfers.push_back(xf(1, me ^ d, cur, slo * ts, (shi - slo) * ts));
+        if (khi > klo) {
+            r.xfers.push_back(xf(0, me ^ d, SCR, soff, (khi - klo) * ts));
+            r.ops.push_back(fold2(DST, klo * ts, cur, klo * ts, SCR, soff, khi - klo));
+        }
+        plan->rounds.push_back(r);
+        stack.push_back(Seg{lo, hi, mid, low});
+        lo = klo;
+        hi = khi;
+        cur = DST;
+    }
+    // recursive doubling: undo the halving in reverse
+    for (int d = pow2 >> 1; d >= 1; d >>= 1) {
+        const Seg parent = stack.back();
+        stack.pop_back();
+        // my range is the half of `parent` I kept; the partner owns the other half
+        const uint64_t olo = parent.low ? parent.mid : parent.lo;
+        const uint64_t ohi = parent.low ? parent.hi : parent.mid;
+        Round r;
+        if (hi > lo) r.xfers.push_back(xf(1, me ^ d, DST, lo * ts, (hi - lo) * ts));
+        if (ohi > olo) r.xfers.push_back(xf(0, me ^ d, DST, olo * ts, (ohi - olo) * ts));
+        plan->rounds.push_back(r);
+        lo = parent.lo;
+        hi = parent.hi;
+    }
+    if (me < P - pow2) {
+        Round b;
+        b.xfers.push_back(xf(1, me + pow2, DST, 0, bytes));
+        plan->rounds.push_back(b);
+    }
+    return SOSX_OK;
+}
+
+}  // namespace
+
+void ring_chunk(uint64_t count, int P, int c, uint64_t *n, uint64_t *first)
+{
+    const uint64_t rem = count % (uint64_t)P;
+    const uint64_t extra = (uint64_t)c < rem;
+    const uint64_t cnt = count / (uint64_t)P + extra;
+    *n = cnt;
+    *first = extra ? (uint64_t)c * cnt : (uint64_t)c * cnt + rem;
+}
+
+int resolve_alg(int alg, uint64_t bytes, uint64_t crossover)
+{
+    if (alg == SOSX_ALG_AUTO) return bytes < crossover ? SOSX_ALG_RECDBL : SOSX_ALG_RING;
+    return alg;
+}
+
+int build(int alg, int P, int me, uint64_t count, uint64_t ts, unsigned src_mis,
+          unsigned dst_mis, Plan *out)
+{
+    if (!out || P < 1 || me < 0 || me >= P || ts == 0) return SOSX_ERR_ARG;
+    out->alg = alg;
+    out->rounds.clear();
+    out->scratch_bytes = 0;
+    if (count == 0) return SOSX_OK;
+    if (P == 1) {
+        // PE_size == 1: the reference copies source to target (src/collectives.c:664-668)
+        Round r;
+        Local l;
+        memset(&l, 0, sizeof(l));
+        l.kind = COPY;
+        l.out_buf = DST;
+        l.nin = 1;
+        l.in_buf[0] = SRC;
+        l.count = count * ts;
+        r.ops.push_back(l);
+        out->rounds.push_back(r);
+        return SOSX_OK;
+    }
+    switch (alg) {
+        case SOSX_ALG_RING:
+        case SOSX_ALG_RECDBL_DIRECT:
+            return build_direct(alg, P, me, count, ts, src_mis, dst_mis, out);
+        case SOSX_ALG_RECDBL:
+            return build_recdbl(P, me, count, ts, dst_mis, out);
+        case SOSX_ALG_RECHALVING:
+            return build_rechalving(P, me, count, ts, dst_mis, out);
+        default:
+            return SOSX_ERR_ARG;
+    }
+}
+
+}  // namespace sosplan
+
+// --------------------------------------------------------------------------------
+// C ABI: plan introspection (CPU tests simulate every PE's plan against the oracle)
+// Encoding (int64 words): [alg, nrounds, scratch_bytes,
+//   per round: nx, nops, nx * (send, peer, buf, off, bytes),
+//              nops * (kind, order, out_buf, out_off, nin, count, nin * (buf, off))]
+// Returns the number of words (the buffer is filled only if cap >= that), or < 0.
+// --------------------------------------------------------------------------------
+extern "C" long long sosx_plan_encode(int alg, int P, int me, unsigned long long count,
+                                      unsigned long long ts, unsigned src_mis,
+                                      unsigned dst_mis, long long *out, unsigned long long cap)
+{
+    sosplan::Plan p;
+    int rc = sosplan::build(alg, P, me, count, ts, src_mis, dst_mis, &p);
+    if (rc) return rc;
+    std::vector<long long> w;
+    w.push_back(p.alg);
+    w.push_back((long long)p.rounds.size());
+    w.push_back((long long)p.scratch_bytes);
+    for (const auto &r : p.rounds) {
+        w.push_back((long long)r.xfers.size());
+        w.push_back((long long)r.ops.size());
+        for (const auto &x : r.xfers) {
+            w.push_back(x.send);
+            w.push_back(x.peer);
+            w.push_back(x.buf);
+            w.push_back((long long)x.off);
+            w.push_back((long long)x.bytes);
+        }
+        for (const auto &l : r.ops) {
+            w.push_back(l.kind);
+            w.push_back(l.order);
+            w.push_back(l.out_buf);
+            w.push_back((long long)l.out_off);
+            w.push_back(l.nin);
+            w.push_back((long long)l.count);
+            for (int k = 0; k < l.nin; ++k) {
+                w.push_back(l.in_buf[k]);
+                w.push_back((long long)l.in_off[k]);
+            }
+        }
+    }
+    if (out && cap >= w.size()) memcpy(out, w.data(), w.size() * sizeof(long long));
+    return (long long)w.size();
+}
+
+extern "C" int sosx_resolve_alg(int alg, unsigned long long bytes, unsigned long long crossover)
+{
+    return sosplan::resolve_alg(alg, bytes, crossover);
+}

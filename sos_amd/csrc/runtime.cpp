@@ -1,0 +1,753 @@
+// runtime.cpp -- init/finalize, symmetric heaps, teams, barriers and diagnostics of
+// the MI355X SOS reduction runtime.  See runtime.h for the design.
+#include "runtime.h"
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+#include <unistd.h>
+
+#include <string>
+
+#include "bootstrap.h"
+#include "shmem.h"
+#include "shmemx.h"
+
+// The executable's data segment, as SOS uses for its symmetric-address check
+// (src/init.c:341-346); weak so a loader without them still links.
+extern "C" char __data_start[] __attribute__((weak));
+extern "C" char _end[] __attribute__((weak));
+
+extern "C" {
+shmem_team_t SHMEM_TEAM_WORLD = nullptr;
+shmem_team_t SHMEM_TEAM_SHARED = nullptr;
+}
+
+namespace sosrt {
+
+State &st()
+{
+    static State s;
+    return s;
+}
+
+// ---------------------------------------------------------------------------------
+// diagnostics (src/shmem_internal.h:60-180)
+// ---------------------------------------------------------------------------------
+void raise_error(const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "[%04d] ERROR: %s\n", st().my_pe, buf);
+    fprintf(stderr, "[%04d] ERROR: Sandia OpenSHMEM (MI355X reduction path) exited in error\n",
+            st().my_pe);
+    fflush(stderr);
+    _exit(1);  // shmem_runtime_abort(1, ...): no atexit handlers, the launcher reaps the job
+}
+
+void warn(const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "[%04d] WARN:  %s\n", st().my_pe, buf);
+}
+
+void debug_msg(const char *fmt, ...)
+{
+    if (!st().debug) return;
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "[%04d] DEBUG: %s\n", st().my_pe, buf);
+}
+
+void check_initialized(const char *fn)
+{
+    if (!st().initialized) raise_error("%s called before shmem_init or after shmem_finalize", fn);
+}
+
+void hip_check(hipError_t e, const char *what)
+{
+    if (e != hipSuccess) raise_error("HIP error in %s: %s", what, hipGetErrorString(e));
+}
+
+void nccl_check(ncclResult_t r, const char *what)
+{
+    if (r != ncclSuccess) raise_error("RCCL error in %s: %s", what, ncclGetErrorString(r));
+}
+
+// ---------------------------------------------------------------------------------
+// environment (src/shmem_env_defs.h, src/shmem_env.c:34-117)
+// ---------------------------------------------------------------------------------
+static size_t atol_scaled(const char *s, size_t dflt)
+{
+    if (!s || !*s) return dflt;
+    char *end = nullptr;
+    double v = strtod(s, &end);
+    if (end == s || v < 0) return dflt;
+    switch (*end) {
+        case 'k': case 'K': v *= 1024.0; break;
+        case 'm': case 'M': v *= 1024.0 * 1024.0; break;
+        case 'g': case 'G': v *= 1024.0 * 1024.0 * 1024.0; break;
+        case 't': case 'T': v *= 1024.0 * 1024.0 * 1024.0 * 1024.0; break;
+        default: break;
+    }
+    return (size_t)v;
+}
+
+static const char *getenv2(const char *name)
+{
+    // SOS accepts SHMEM_<X> and SMA_<X> (src/shmem_env.c:90-117)
+    const char *v = getenv((std::string("SHMEM_") + name).c_str());
+    if (!v) v = getenv((std::string("SMA_") + name).c_str());
+    return v;
+}
+
+int parse_reduce_alg(const char *type, int dflt)
+{
+    if (!type) return dflt;
+    if (!strcmp(type, "auto")) return SOSX_ALG_AUTO;
+    // linear and tree need NIC atomics; without them SOS runs recdbl_sw
+    // (src/shmem_collectives.h:200-221)
+    if (!strcmp(type, "linear") || !strcmp(type, "tree") || !strcmp(type, "recdbl"))
+        return SOSX_ALG_RECDBL;
+    if (!strcmp(type, "ring")) return SOSX_ALG_RING;
+    if (!strcmp(type, "rechalving")) return SOSX_ALG_RECHALVING;
+    if (!strcmp(type, "recdbl_direct")) return SOSX_ALG_RECDBL_DIRECT;
+    warn("Ignoring bad reduction algorithm '%s'", type);
+    return dflt;
+}
+
+static void read_env(State &s)
+{
+    s.reduce_alg = parse_reduce_alg(getenv2("REDUCE_ALGORITHM"), SOSX_ALG_AUTO);
+    s.coll_size_crossover = atol_scaled(getenv2("COLL_SIZE_CROSSOVER"), 16384);
+    s.symmetric_size = atol_scaled(getenv2("SYMMETRIC_SIZE"), 512u << 20);
+    const char *d = getenv2("DEBUG");
+    s.debug = d && *d && strcmp(d, "0") && strcasecmp(d, "false");
+    const char *h = getenv("SHMEMX_HEAP_ON_DEVICE");
+    s.heap_on_device = h && *h && strcmp(h, "0");
+    const char *c = getenv("SHMEMX_CHECK_SYMMETRIC");
+    s.error_checking = c && *c && strcmp(c, "0");
+}
+
+// ---------------------------------------------------------------------------------
+// symmetric heaps: first-fit allocator over one region (same call sequence on every
+// PE => same offsets, as SOS's dlmalloc heap at a fixed base, src/malloc.c)
+// ---------------------------------------------------------------------------------
+void Heap::init(char *b, size_t s, bool dev, bool ext)
+{
+    base = b;
+    size = s;
+    device = dev;
+    external = ext;
+    free_blocks.clear();
+    used_blocks.clear();
+    free_blocks[0] = s;
+}
+
+void *Heap::alloc(size_t bytes, size_t align)
+{
+    if (!base) return nullptr;
+    if (align < 256) align = 256;
+    if (bytes == 0) bytes = 1;
+    bytes = (bytes + 255) & ~(size_t)255;
+    for (auto it = free_blocks.begin(); it != free_blocks.end(); ++it) {
+        size_t off = it->first, len = it->second;
+        size_t aoff = (off + align - 1) / align * align;
+        if (aoff + bytes > off + len) continue;
+        free_blocks.erase(it);
+        if (aoff > off) free_blocks[off] = aoff - off;
+        if (off + len > aoff + bytes) free_blocks[aoff + bytes] = off + len - (aoff + bytes);
+        used_blocks[aoff] = bytes;
+        return base + aoff;
+    }
+    return nullptr;
+}
+
+bool Heap::release(void *p)
+{
+    if (!contains(p, 1)) return false;
+    size_t off = (size_t)((char *)p - base);
+    auto u = used_blocks.find(off);
+    if (u == used_blocks.end()) return false;
+    size_t len = u->second;
+    used_blocks.erase(u);
+    auto nx = free_blocks.lower_bound(off);
+    if (nx != free_blocks.end() && nx->first == off + len) {
+        len += nx->second;
+        free_blocks.erase(nx);
+    }
+    auto pv = free_blocks.lower_bound(off);
+    if (pv != free_blocks.begin()) {
+        --pv;
+        if (pv->first + pv->second == off) {
+            pv->second += len;
+            return true;
+        }
+    }
+    free_blocks[off] = len;
+    return true;
+}
+
+static void ensure_host_heap(State &s)
+{
+    if (s.host_heap.base) return;
+    void *p = nullptr;
+    hip_check(hipHostMalloc(&p, s.symmetric_size, hipHostMallocDefault), "hipHostMalloc(heap)");
+    s.host_heap.init((char *)p, s.symmetric_size, false, false);
+}
+
+static void ensure_device_heap(State &s)
+{
+    if (s.dev_heap.base) return;
+    void *p = nullptr;
+    hip_check(hipMalloc(&p, s.symmetric_size), "hipMalloc(device heap)");
+    s.dev_heap.init((char *)p, s.symmetric_size, true, false);
+}
+
+// ---------------------------------------------------------------------------------
+// device workspaces
+// ---------------------------------------------------------------------------------
+static void *grow(void **buf, size_t *have, size_t need, const char *what)
+{
+    if (need <= *have && *buf) return *buf;
+    State &s = st();
+    if (*buf) {
+        hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize");
+        hip_check(hipFree(*buf), "hipFree");
+        *buf = nullptr;
+    }
+    size_t sz = need < (1u << 20) ? (1u << 20) : need;
+    hip_check(hipMalloc(buf, sz), what);
+    *have = sz;
+    return *buf;
+}
+
+void *scratch(size_t bytes) { return grow(&st().scratch, &st().scratch_bytes, bytes, "hipMalloc(scratch)"); }
+void *stage(size_t bytes) { return grow(&st().stage, &st().stage_bytes, bytes, "hipMalloc(stage)"); }
+
+bool is_device_ptr(const void *p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // pageable host memory: not registered with HIP
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+bool is_symmetric(const void *p, size_t bytes)
+{
+    State &s = st();
+    if (s.host_heap.contains(p, bytes) || s.dev_heap.contains(p, bytes)) return true;
+    if (__data_start && _end && (const char *)p >= __data_start && (const char *)p + bytes <= _end)
+        return true;
+    for (auto &kv : s.dev_allocs)
+        if ((const char *)p >= (char *)kv.first && (const char *)p + bytes <= (char *)kv.first + kv.second)
+            return true;
+    if (s.ext_base && (const char *)p >= (char *)s.ext_base &&
+        (const char *)p + bytes <= (char *)s.ext_base + s.ext_size)
+        return true;
+    return false;
+}
+
+// ---------------------------------------------------------------------------------
+// barriers: dissemination over RCCL point-to-point (ceil(log2 P) rounds), so any
+// strided team can synchronise without a communicator of its own
+// ---------------------------------------------------------------------------------
+void team_barrier(const Team &t)
+{
+    State &s = st();
+    if (t.size > 1 && t.my_idx >= 0) {
+        for (int d = 1; d < t.size; d <<= 1) {
+            const int to = t.world_rank((t.my_idx + d) % t.size);
+            const int from = t.world_rank((t.my_idx - d + t.size) % t.size);
+            nccl_check(ncclGroupStart(), "ncclGroupStart");
+            nccl_check(ncclSend(s.dbar, 1, ncclInt32, to, s.comm, s.stream), "ncclSend(barrier)");
+            nccl_check(ncclRecv(s.dbar + 1, 1, ncclInt32, from, s.comm, s.stream), "ncclRecv(barrier)");
+            nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+        }
+    }
+    hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize(barrier)");
+}
+
+Team *team_from_handle(void *handle) { return (Team *)handle; }
+
+// ---------------------------------------------------------------------------------
+// init (src/init.c:221-567, condensed to what the reduction path needs)
+// ---------------------------------------------------------------------------------
+static void init_common(int pe, int npes, const ncclUniqueId &uid)
+{
+    State &s = st();
+    read_env(s);
+    s.my_pe = pe;
+    s.n_pes = npes;
+    int ndev = 0;
+    hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    if (ndev < 1) raise_error("no AMD GPU visible: this SOS build runs the reduction path on HIP");
+    const char *dv = getenv("SHMEMX_DEVICE");
+    s.device = dv ? atoi(dv) : sosboot::local_rank(pe) % ndev;
+    hip_check(hipSetDevice(s.device), "hipSetDevice");
+    hip_check(hipStreamCreateWithFlags(&s.own_stream, hipStreamNonBlocking), "hipStreamCreate");
+    s.stream = s.own_stream;
+    hip_check(hipMalloc((void **)&s.dbar, 64), "hipMalloc(barrier word)");
+    hip_check(hipMemset(s.dbar, 0, 64), "hipMemset");
+    nccl_check(ncclCommInitRank(&s.comm, npes, uid, pe), "ncclCommInitRank");
+    if (s.ext_base) s.dev_heap.init((char *)s.ext_base, s.ext_size, true, true);
+    s.world = Team();
+    s.world.start = 0;
+    s.world.stride = 1;
+    s.world.size = npes;
+    s.world.my_idx = pe;
+    s.world.valid = true;
+    s.world.predefined = true;
+    s.shared = s.world;  // one node: every PE shares it
+    SHMEM_TEAM_WORLD = &s.world;
+    SHMEM_TEAM_SHARED = &s.shared;
+    s.initialized = true;
+    s.finalized = false;
+    debug_msg("PE %d of %d on device %d, reduce algorithm %d, crossover %zu", pe, npes, s.device,
+              s.reduce_alg, s.coll_size_crossover);
+    team_barrier(s.world);
+}
+
+}  // namespace sosrt
+
+using namespace sosrt;
+
+extern "C" {
+
+void shmem_init(void)
+{
+    State &s = st();
+    if (s.initialized) return;
+    int rank, size;
+    sosboot::discover(&rank, &size);
+    ncclUniqueId uid;
+    memset(&uid, 0, sizeof(uid));
+    if (rank == 0) nccl_check(ncclGetUniqueId(&uid), "ncclGetUniqueId");
+    char host[64] = {0}, err[256] = {0};
+    gethostname(host, sizeof(host) - 1);
+    std::string recs((size_t)size * sizeof(host), '\0');
+    if (sosboot::exchange(rank, size, &uid, sizeof(uid), &uid, host, sizeof(host), &recs[0], err,
+                          sizeof(err)) != 0) {
+        s.my_pe = rank;
+        raise_error("shmem_init: %s", err);
+    }
+    for (int r = 0; r < size; ++r)
+        if (strncmp(&recs[(size_t)r * sizeof(host)], host, sizeof(host)) != 0)
+            raise_error("shmem_init: PE %d runs on another node; this build is single-node "
+                        "(one PE per MI355X over xGMI)", r);
+    init_common(rank, size, uid);
+}
+
+int shmem_init_thread(int requested, int *provided)
+{
+    shmem_init();
+    // collectives are serialised by the caller, as in SOS (pSync selection is unlocked)
+    st().thread_level = requested > SHMEM_THREAD_SERIALIZED ? SHMEM_THREAD_SERIALIZED : requested;
+    if (provided) *provided = st().thread_level;
+    return 0;
+}
+
+void shmem_query_thread(int *provided)
+{
+    if (provided) *provided = st().thread_level;
+}
+
+int shmemx_get_unique_id(void *uid, size_t len)
+{
+    if (!uid || len < sizeof(ncclUniqueId)) return SOSX_ERR_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return SOSX_ERR_RCCL;
+    memcpy(uid, &id, sizeof(id));
+    return SOSX_OK;
+}
+
+int shmemx_init_attr(int my_pe, int n_pes, const void *uid, size_t len)
+{
+    if (st().initialized) return SOSX_ERR_STATE;
+    if (!uid || len < sizeof(ncclUniqueId) || n_pes < 1 || my_pe < 0 || my_pe >= n_pes)
+        return SOSX_ERR_ARG;
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof(id));
+    init_common(my_pe, n_pes, id);
+    return SOSX_OK;
+}
+
+void shmem_finalize(void)
+{
+    State &s = st();
+    if (!s.initialized) return;
+    team_barrier(s.world);
+    if (s.comm) ncclCommDestroy(s.comm);
+    s.comm = nullptr;
+    if (s.scratch) (void)hipFree(s.scratch);
+    if (s.stage) (void)hipFree(s.stage);
+    if (s.dbar) (void)hipFree(s.dbar);
+    s.scratch = s.stage = nullptr;
+    s.scratch_bytes = s.stage_bytes = 0;
+    s.dbar = nullptr;
+    if (s.host_heap.base) (void)hipHostFree(s.host_heap.base);
+    if (s.dev_heap.base && !s.dev_heap.external) (void)hipFree(s.dev_heap.base);
+    s.host_heap = Heap();
+    s.dev_heap = Heap();
+    for (auto &kv : s.dev_allocs) (void)hipFree(kv.first);
+    s.dev_allocs.clear();
+    if (s.own_stream) (void)hipStreamDestroy(s.own_stream);
+    s.own_stream = s.stream = nullptr;
+    s.initialized = false;
+    s.finalized = true;
+}
+
+void shmem_global_exit(int status)
+{
+    fflush(stdout);
+    fflush(stderr);
+    _exit(status);
+}
+
+int shmem_my_pe(void) { return st().initialized ? st().my_pe : -1; }
+int shmem_n_pes(void) { return st().initialized ? st().n_pes : -1; }
+
+int shmem_pe_accessible(int pe) { return st().initialized && pe >= 0 && pe < st().n_pes; }
+
+int shmem_addr_accessible(const void *addr, int pe)
+{
+    return shmem_pe_accessible(pe) && is_symmetric(addr, 1);
+}
+
+void shmem_info_get_version(int *major, int *minor)
+{
+    if (major) *major = SHMEM_MAJOR_VERSION;
+    if (minor) *minor = SHMEM_MINOR_VERSION;
+}
+
+void shmem_info_get_name(char *name)
+{
+    if (name) {
+        strncpy(name, SHMEM_VENDOR_STRING, SHMEM_MAX_NAME_LEN - 1);
+        name[SHMEM_MAX_NAME_LEN - 1] = 0;
+    }
+}
+
+// ---- symmetric memory (src/symmetric_heap_c.c:285-432: allocation + barrier) ----
+void *shmem_malloc(size_t size)
+{
+    check_initialized("shmem_malloc");
+    State &s = st();
+    void *p;
+    {
+        std::lock_guard<std::mutex> g(s.mu);
+        if (s.heap_on_device) {
+            ensure_device_heap(s);
+            p = s.dev_heap.alloc(size, 256);
+        } else {
+            ensure_host_heap(s);
+            p = s.host_heap.alloc(size, 256);
+        }
+    }
+    if (!p && size)
+        raise_error("shmem_malloc(%zu): symmetric heap exhausted (SHMEM_SYMMETRIC_SIZE=%zu)", size,
+                    s.symmetric_size);
+    team_barrier(s.world);
+    return p;
+}
+
+void *shmem_calloc(size_t count, size_t size)
+{
+    void *p = shmem_malloc(count * size);
+    if (p) {
+        if (st().heap_on_device)
+            hip_check(hipMemset(p, 0, count * size), "hipMemset");
+        else
+            memset(p, 0, count * size);
+    }
+    return p;
+}
+
+void *shmem_align(size_t alignment, size_t size)
+{
+    check_initialized("shmem_align");
+    State &s = st();
+    if (alignment == 0 || (alignment & (alignment - 1))) return nullptr;
+    void *p;
+    {
+        std::lock_guard<std::mutex> g(s.mu);
+        Heap &h = s.heap_on_device ? s.dev_heap : s.host_heap;
+        if (s.heap_on_device) ensure_device_heap(s); else ensure_host_heap(s);
+        p = h.alloc(size, alignment);
+    }
+    team_barrier(s.world);
+    return p;
+}
+
+void shmem_free(void *ptr)
+{
+    if (!ptr) return;
+    check_initialized("shmem_free");
+    State &s = st();
+    team_barrier(s.world);
+    std::lock_guard<std::mutex> g(s.mu);
+    if (!s.host_heap.release(ptr) && !s.dev_heap.release(ptr))
+        raise_error("shmem_free: %p is not a symmetric heap address", ptr);
+}
+
+void *shmem_realloc(void *ptr, size_t size)
+{
+    if (!ptr) return shmem_malloc(size);
+    if (size == 0) {
+        shmem_free(ptr);
+        return nullptr;
+    }
+    State &s = st();
+    Heap &h = s.host_heap.contains(ptr, 1) ? s.host_heap : s.dev_heap;
+    size_t old = 0;
+    {
+        auto it = h.used_blocks.find((size_t)((char *)ptr - h.base));
+        if (it == h.used_blocks.end()) raise_error("shmem_realloc: %p is not a heap address", ptr);
+        old = it->second;
+    }
+    void *np = shmem_malloc(size);
+    size_t n = old < size ? old : size;
+    if (h.device)
+        hip_check(hipMemcpy(np, ptr, n, hipMemcpyDeviceToDevice), "hipMemcpy");
+    else
+        memcpy(np, ptr, n);
+    shmem_free(ptr);
+    return np;
+}
+
+void *shmemx_malloc_device(size_t size)
+{
+    check_initialized("shmemx_malloc_device");
+    State &s = st();
+    void *p = nullptr;
+    hip_check(hipMalloc(&p, size ? size : 1), "hipMalloc(shmemx_malloc_device)");
+    {
+        std::lock_guard<std::mutex> g(s.mu);
+        s.dev_allocs[p] = size;
+    }
+    team_barrier(s.world);
+    return p;
+}
+
+void shmemx_free_device(void *ptr)
+{
+    if (!ptr) return;
+    State &s = st();
+    team_barrier(s.world);
+    std::lock_guard<std::mutex> g(s.mu);
+    auto it = s.dev_allocs.find(ptr);
+    if (it == s.dev_allocs.end()) raise_error("shmemx_free_device: %p was not allocated by shmemx_malloc_device", ptr);
+    s.dev_allocs.erase(it);
+    hip_check(hipFree(ptr), "hipFree");
+}
+
+void shmemx_heap_create(void *base, size_t size, int device_type, int device_index)
+{
+    State &s = st();
+    if (s.initialized) {
+        warn("Ignoring pre-setup. Heap already initialized");
+        return;
+    }
+    if (!base || size == 0 || device_type != SHMEMX_EXTERNAL_HEAP_HIP)
+        raise_error("shmemx_heap_create: this build accepts HIP device heaps "
+                    "(SHMEMX_EXTERNAL_HEAP_HIP) only");
+    (void)device_index;
+    s.ext_base = base;
+    s.ext_size = size;
+    s.ext_type = device_type;
+}
+
+void shmemx_set_stream(void *hip_stream)
+{
+    State &s = st();
+    s.stream = hip_stream ? (hipStream_t)hip_stream : s.own_stream;
+}
+
+void *shmemx_get_stream(void) { return (void *)st().stream; }
+
+int shmemx_get_device(void) { return st().device; }
+
+int shmemx_set_reduce_algorithm(int alg)
+{
+    int prev = st().reduce_alg;
+    if (alg >= SOSX_ALG_AUTO && alg <= SOSX_ALG_RECDBL_DIRECT) st().reduce_alg = alg;
+    return prev;
+}
+
+// ---- synchronisation -------------------------------------------------------------
+void shmem_barrier_all(void)
+{
+    check_initialized("shmem_barrier_all");
+    team_barrier(st().world);
+}
+
+void shmem_sync_all(void) { shmem_barrier_all(); }
+
+void shmem_quiet(void)
+{
+    if (st().initialized) hip_check(hipStreamSynchronize(st().stream), "hipStreamSynchronize");
+}
+
+void shmem_fence(void) { shmem_quiet(); }
+
+static Team active_set(int PE_start, int logPE_stride, int PE_size, const char *fn)
+{
+    State &s = st();
+    const int stride = 1 << logPE_stride;
+    // SHMEM_ERR_CHECK_ACTIVE_SET (src/shmem_internal.h:214-227)
+    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) > s.n_pes)
+        raise_error("%s: Invalid active set (PE_start = %d, PE_stride = %d, PE_size = %d)", fn,
+                    PE_start, stride, PE_size);
+    if (!(s.my_pe >= PE_start && s.my_pe <= PE_start + ((PE_size - 1) * stride) &&
+          (s.my_pe - PE_start) % stride == 0))
+        raise_error("%s: Calling PE (%d) is not a member of the active set", fn, s.my_pe);
+    Team t;
+    t.start = PE_start;
+    t.stride = stride;
+    t.size = PE_size;
+    t.my_idx = (s.my_pe - PE_start) / stride;
+    t.valid = true;
+    return t;
+}
+
+void shmem_sync(int PE_start, int logPE_stride, int PE_size, long *pSync)
+{
+    check_initialized("shmem_sync");
+    (void)pSync;
+    team_barrier(active_set(PE_start, logPE_stride, PE_size, "shmem_sync"));
+}
+
+void shmem_barrier(int PE_start, int logPE_stride, int PE_size, long *pSync)
+{
+    shmem_sync(PE_start, logPE_stride, PE_size, pSync);
+}
+
+// ---- teams (src/shmem_team.c, src/teams_c.c4) -------------------------------------
+static Team *team_checked(shmem_team_t team, const char *fn)
+{
+    check_initialized(fn);
+    Team *t = team_from_handle(team);
+    if (!t || !t->valid) raise_error("%s: invalid team", fn);  // SHMEM_ERR_CHECK_TEAM_VALID
+    return t;
+}
+
+int shmem_team_my_pe(shmem_team_t team)
+{
+    if (team == SHMEM_TEAM_INVALID) return -1;
+    return team_checked(team, "shmem_team_my_pe")->my_idx;
+}
+
+int shmem_team_n_pes(shmem_team_t team)
+{
+    if (team == SHMEM_TEAM_INVALID) return -1;
+    return team_checked(team, "shmem_team_n_pes")->size;
+}
+
+int shmem_team_get_config(shmem_team_t team, long config_mask, shmem_team_config_t *config)
+{
+    team_checked(team, "shmem_team_get_config");
+    if (config && (config_mask & SHMEM_TEAM_NUM_CONTEXTS)) config->num_contexts = 0;
+    return 0;
+}
+
+int shmem_team_translate_pe(shmem_team_t src_team, int src_pe, shmem_team_t dest_team)
+{
+    if (src_team == SHMEM_TEAM_INVALID || dest_team == SHMEM_TEAM_INVALID) return -1;
+    Team *s = team_checked(src_team, "shmem_team_translate_pe");
+    Team *d = team_checked(dest_team, "shmem_team_translate_pe");
+    if (src_pe < 0 || src_pe >= s->size) return -1;
+    const int g = s->world_rank(src_pe);
+    if (g < d->start || (g - d->start) % d->stride) return -1;
+    const int idx = (g - d->start) / d->stride;
+    return idx < d->size ? idx : -1;
+}
+
+int shmem_team_split_strided(shmem_team_t parent_team, int PE_start, int PE_stride, int PE_size,
+                             const shmem_team_config_t *config, long config_mask,
+                             shmem_team_t *new_team)
+{
+    (void)config;
+    (void)config_mask;
+    Team *parent = team_checked(parent_team, "shmem_team_split_strided");
+    if (new_team) *new_team = SHMEM_TEAM_INVALID;
+    // argument rules of src/shmem_team.c:300-321
+    if (PE_start < 0 || PE_start >= parent->size || PE_size <= 0 || PE_size > parent->size ||
+        PE_stride < 1 || PE_start + (PE_size - 1) * PE_stride >= parent->size) {
+        warn("Invalid <start, stride, size>: child <%d, %d, %d>, parent <%d, %d, %d>", PE_start,
+             PE_stride, PE_size, parent->start, parent->stride, parent->size);
+        team_barrier(*parent);
+        return -1;
+    }
+    Team child;
+    child.start = parent->world_rank(PE_start);
+    child.stride = parent->stride * PE_stride;
+    child.size = PE_size;
+    child.valid = true;
+    const int my = parent->my_idx;
+    if (my >= PE_start && (my - PE_start) % PE_stride == 0 && (my - PE_start) / PE_stride < PE_size) {
+        child.my_idx = (my - PE_start) / PE_stride;
+        if (new_team) *new_team = new Team(child);
+    }
+    team_barrier(*parent);
+    return 0;
+}
+
+int shmem_team_split_2d(shmem_team_t parent_team, int xrange, const shmem_team_config_t *xaxis_config,
+                        long xaxis_mask, shmem_team_t *xaxis_team,
+                        const shmem_team_config_t *yaxis_config, long yaxis_mask,
+                        shmem_team_t *yaxis_team)
+{
+    // src/shmem_team.c:436-505: x teams are consecutive runs of xrange PEs, y teams
+    // stride xrange through the parent.
+    Team *parent = team_checked(parent_team, "shmem_team_split_2d");
+    if (xrange <= 0) {
+        warn("Invalid xrange (%d)", xrange);
+        return -1;
+    }
+    if (xrange > parent->size) xrange = parent->size;
+    const int my = parent->my_idx;
+    const int xstart = my / xrange * xrange;
+    const int xsize = (parent->size - xstart) < xrange ? parent->size - xstart : xrange;
+    int rc = shmem_team_split_strided(parent_team, xstart, 1, xsize, xaxis_config, xaxis_mask,
+                                      xaxis_team);
+    // every PE must take part in every split of the parent: run all x splits in order
+    (void)rc;
+    const int ystart = my % xrange;
+    const int ysize = (parent->size - ystart + xrange - 1) / xrange;
+    rc = shmem_team_split_strided(parent_team, ystart, xrange, ysize, yaxis_config, yaxis_mask,
+                                  yaxis_team);
+    return rc;
+}
+
+void shmem_team_destroy(shmem_team_t team)
+{
+    Team *t = team_from_handle(team);
+    if (!t || t->predefined) return;
+    t->valid = false;
+    delete t;
+}
+
+int shmem_team_sync(shmem_team_t team)
+{
+    if (team == SHMEM_TEAM_INVALID) return -1;
+    team_barrier(*team_checked(team, "shmem_team_sync"));
+    return 0;
+}
+
+}  // extern "C"

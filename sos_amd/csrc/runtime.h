@@ -1,0 +1,118 @@
+// runtime.h -- process-wide state of the MI355X SOS reduction runtime.
+//
+// One PE = one process = one GPU (device = LOCAL_RANK, else pe % device count).
+// What SOS's init (src/init.c:221-550) sets up for the reduction path, rebuilt
+// MI355X-first:
+//   * rank/size discovery + a TCP bootstrap that broadcasts the RCCL unique id
+//     (replaces the PMI KVS exchange of src/runtime-pmi.c);
+//   * one RCCL communicator over all PEs (xGMI peer links on one node), carrying
+//     every inter-PE byte of the team reductions (replaces the one-sided put/atomic
+//     layer, src/shmem_comm.h, and the XPMEM/CMA/OFI transports);
+//   * one non-blocking HIP stream per PE on which RCCL transfers and the combine
+//     kernels are ordered (no host round trip between schedule steps);
+//   * symmetric heaps: pinned host memory (shmem_malloc, SOS semantics: CPU
+//     accessible, src/symmetric_heap_c.c) and device HBM (shmemx_malloc_device /
+//     shmemx_heap_create with SHMEMX_EXTERNAL_HEAP_HIP);
+//   * teams (start, stride, size) with SOS's pSync bookkeeping.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+
+#include "sosx.h"
+
+namespace sosrt {
+
+struct Team {
+    int start = 0, stride = 1, size = 1;
+    int my_idx = -1;          // index of this PE in the team, -1 if not a member
+    int psync_avail[2] = {1, 1};  // SOS N_PSYNCS_PER_TEAM (src/shmem_team.h:18)
+    bool valid = false;
+    bool predefined = false;
+    int world_rank(int idx) const { return start + idx * stride; }
+};
+
+struct Heap {
+    char *base = nullptr;
+    size_t size = 0;
+    bool device = false;
+    bool external = false;
+    std::map<size_t, size_t> free_blocks;  // offset -> size
+    std::map<size_t, size_t> used_blocks;  // offset -> size
+    void init(char *b, size_t s, bool dev, bool ext);
+    void *alloc(size_t bytes, size_t align);
+    bool release(void *p);
+    bool contains(const void *p, size_t bytes) const
+    {
+        return base && (const char *)p >= base && (const char *)p + bytes <= base + size;
+    }
+};
+
+struct State {
+    bool initialized = false;
+    bool finalized = false;
+    int my_pe = 0;
+    int n_pes = 1;
+    int device = 0;
+    int thread_level = 0;
+    hipStream_t stream = nullptr;     // library stream (or the user's, shmemx_set_stream)
+    hipStream_t own_stream = nullptr;
+    ncclComm_t comm = nullptr;
+    // device workspaces, grown on demand
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    void *stage = nullptr;            // staging for host-resident source/target
+    size_t stage_bytes = 0;
+    int *dbar = nullptr;              // 1-int device word for barriers
+    Heap host_heap;                   // shmem_malloc (pinned host)
+    Heap dev_heap;                    // shmemx_malloc_device / external HIP heap
+    std::map<void *, size_t> dev_allocs;  // direct device allocations (no heap)
+    // external heap registered before init (shmemx_heap_create)
+    void *ext_base = nullptr;
+    size_t ext_size = 0;
+    int ext_type = -1;
+    // parameters (SOS env table subset, src/shmem_env_defs.h)
+    int reduce_alg = SOSX_ALG_AUTO;
+    size_t coll_size_crossover = 16384;
+    size_t symmetric_size = 512u << 20;
+    bool debug = false;
+    bool error_checking = true;
+    bool heap_on_device = false;
+    // teams
+    Team world, shared;
+    std::mutex mu;
+};
+
+State &st();
+
+// Abort the job with an SOS-style message ("[%04d] ERROR: ..."), like RAISE_ERROR_MSG
+// (src/shmem_internal.h:124-128) -> shmem_runtime_abort.
+[[noreturn]] void raise_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+void warn(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+void debug_msg(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+
+void check_initialized(const char *fn);
+void hip_check(hipError_t e, const char *what);
+void nccl_check(ncclResult_t r, const char *what);
+
+// Device workspaces (grown, never shrunk).
+void *scratch(size_t bytes);
+void *stage(size_t bytes);
+
+// Is `p` a device (HBM) pointer?  Host pageable, pinned and static data are not.
+bool is_device_ptr(const void *p);
+
+// Symmetric check (SHMEM_ERR_CHECK_SYMMETRIC, src/shmem_internal.h:250-290).
+bool is_symmetric(const void *p, size_t bytes);
+
+// Barrier across a team: dissemination over RCCL point-to-point, host-synchronous.
+void team_barrier(const Team &t);
+
+Team *team_from_handle(void *handle);
+
+}  // namespace sosrt

@@ -1,0 +1,38 @@
+"""Shared pytest setup.
+
+`-m gpu` tests need an MI355X (they call the HIP path through the C ABI);
+everything else runs on CPU.  The oracle (oracle/) is the checker only.
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X) and libsos_amd.so")
+
+
+@pytest.fixture(scope="session")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test collected but no GPU is visible")
+    return torch
+
+
+@pytest.fixture(scope="session")
+def sos():
+    from sos_amd import _lib
+    _lib.lib()  # raises if the library is missing: no silent fallback
+    return _lib
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as O
+    O.lib()
+    return O

@@ -1,0 +1,124 @@
+"""CPU: the C-ABI library loads, exports every function include/*.h declares, the
+generated bindings are current, and SOS programs compile against include/shmem.h."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include")
+LIB = os.path.join(ROOT, "sos_amd", "libsos_amd.so")
+REF_PI = "/root/reference/examples/pi_reduce.c"
+
+
+def declared_functions():
+    names = set()
+    for h in ("shmem.h", "shmemx.h", "sosx.h", "shmem_reductions.h"):
+        text = open(os.path.join(INC, h)).read()
+        text = text.split("#if defined(__cplusplus)\nstatic inline")[0]  # skip inline overloads
+        for m in re.finditer(r"^\s*(?:SHMEM_FUNCTION_ATTRIBUTES\s+)?(?:const\s+)?[\w ]+?\**\s*\b(\w+)\(",
+                             text, re.M):
+            name = m.group(1)
+            if name.startswith(("shmem", "pshmem", "sosx")) and not name.startswith("SHMEM"):
+                names.add(name)
+    return names
+
+
+def exported_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if len(ln.split()) == 3}
+
+
+def test_library_loads_and_exports_everything():
+    from sos_amd import _lib
+    _lib.lib()
+    declared = declared_functions()
+    assert len(declared) > 400  # 198 shmem_* + 198 pshmem_* reductions + runtime + sosx
+    missing = sorted(declared - exported_symbols())
+    assert not missing, missing
+
+
+def test_198_reduction_symbols():
+    sys.path.insert(0, os.path.join(ROOT, "sos_amd", "csrc"))
+    import gen_bindings
+    names = gen_bindings.symbols()
+    assert len(names) == 198 and len(set(names)) == 198
+    exp = exported_symbols()
+    assert all(n in exp and "p" + n in exp for n in names)
+    # SOS quirks carried over: uint8..64 reduce with the SIGNED internal type
+    src = open(os.path.join(ROOT, "sos_amd", "csrc", "reductions_gen.cpp")).read()
+    assert 'SOSX_OP_MAX, SOSX_DT_INT32, "shmem_uint32_max_reduce"' in src
+    assert 'SOSX_OP_MIN, SOSX_DT_INT8, "shmem_uint8_min_reduce"' in src
+    assert 'SOSX_OP_MAX, SOSX_DT_UCHAR, "shmem_uchar_max_reduce"' in src
+
+
+def test_generated_bindings_current():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "sos_amd", "csrc", "gen_bindings.py"),
+                        "--check"])
+    assert r.returncode == 0
+
+
+def test_constants_match_sos():
+    text = open(os.path.join(INC, "shmem.h")).read()
+    for name, val in (("SHMEM_REDUCE_SYNC_SIZE", 35), ("SHMEM_BCAST_SYNC_SIZE", 1),
+                      ("SHMEM_BARRIER_SYNC_SIZE", 16), ("SHMEM_COLLECT_SYNC_SIZE", 18),
+                      ("SHMEM_SYNC_SIZE", 35), ("SHMEM_REDUCE_MIN_WRKDATA_SIZE", 1),
+                      ("SHMEM_SYNC_VALUE", 0)):
+        assert re.search(rf"#define {name} {val}\b", text), name
+
+
+def _compile(src, lang, tmp_path, extra=()):
+    exe = str(tmp_path / "a.out")
+    cc = "gcc" if lang == "c" else "g++"
+    std = ["-std=gnu11"] if lang == "c" else ["-std=c++17"]
+    cmd = [cc, *std, "-Wall", "-I", INC, "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", src, "-o",
+           exe, "-L", os.path.dirname(LIB), "-lsos_amd", f"-Wl,-rpath,{os.path.dirname(LIB)}",
+           "-L/opt/rocm/lib", "-lamdhip64", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+@pytest.mark.skipif(not os.path.exists(REF_PI), reason="reference checkout not present")
+def test_reference_pi_reduce_compiles_unchanged(tmp_path):
+    """examples/pi_reduce.c (shmem_sum_reduce C11 generic on long long) builds as-is."""
+    _compile(REF_PI, "c", tmp_path)
+
+
+def test_own_examples_compile(tmp_path):
+    for f in ("pi_reduce_amd.c", "reduce_types.c"):
+        _compile(os.path.join(ROOT, "examples", f), "c", tmp_path)
+
+
+def test_cxx_overloads_compile(tmp_path):
+    src = tmp_path / "t.cpp"
+    src.write_text('#include <shmem.h>\nint main(){ shmem_init(); static long long a, b; '
+                   'static double d[4], e[4]; static unsigned u[3], v[3];\n'
+                   'shmem_sum_reduce(SHMEM_TEAM_WORLD, &a, &b, 1); shmem_max_reduce(SHMEM_TEAM_WORLD, d, e, 4);\n'
+                   'shmem_xor_reduce(SHMEM_TEAM_WORLD, u, v, 3); shmem_finalize(); return 0; }\n')
+    _compile(str(src), "cxx", tmp_path)
+
+
+def test_plan_abi_rejects_bad_args():
+    from sos_amd import shmem as S
+    L = S.lib()
+    assert L.sosx_plan_encode(2, 0, 0, 10, 4, 0, 0, None, 0) < 0       # P = 0
+    assert L.sosx_plan_encode(2, 4, 4, 10, 4, 0, 0, None, 0) < 0       # me out of range
+    assert L.sosx_plan_encode(9, 4, 0, 10, 4, 0, 0, None, 0) < 0       # bad algorithm
+    assert L.sosx_plan_encode(2, 4, 0, 0, 4, 0, 0, None, 0) == 3       # count 0: no rounds
+
+
+def test_combine_status_codes_without_gpu():
+    """Argument/type validation happens before any device work."""
+    from sos_amd import _lib
+    L = _lib.lib()
+    assert L.sosx_check_op(5, 23) == 0
+    assert L.sosx_check_op(0, 23) == -2     # and on float: FP class
+    assert L.sosx_check_op(3, 26) == -2     # min on complex
+    assert L.sosx_check_op(5, 0) == -1      # SIGNED_BYTE is not reducible
+    assert L.sosx_check_op(5, 25) == 0      # long double is valid in SOS ...
+    assert L.sosx_combine(5, 25, None, None, 0, None) == 0   # ... (count 0: nothing to do)
+    assert L.sosx_dtype_size(27) == 16 and L.sosx_dtype_size(25) == 16

@@ -1,0 +1,204 @@
+"""GPU parity of the local combine and the fused fold against the CPU oracle.
+
+The oracle (oracle/sos_oracle.c) restates shmem_internal_reduce_local
+(src/shmem_internal_op.h:305-339) and the ring / recdbl schedules
+(src/collectives.c:647-764, :850-984).  Every (datatype, op) pair SOS accepts is
+checked bit for bit, over ragged sizes, misaligned starts and special fp values
+(NaN, +-0, +-inf, denormals), plus the Annex G complex-multiply recovery.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# (datatype id, name) for every reducible shm_internal_datatype_t except long double
+FP_CLASS = [1, 2, 12, 23, 24]            # char, schar, ptrdiff_t, float, double
+CPLX_CLASS = [26, 27]                    # complexf, complexd
+INT_CLASS = [3, 4, 5, 6, 8, 9, 10, 11, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22]
+OPS_FP = [3, 4, 5, 6]
+OPS_CPLX = [5, 6]
+OPS_INT = [0, 1, 2, 3, 4, 5, 6]
+PAIRS = ([(d, o) for d in FP_CLASS for o in OPS_FP] + [(d, o) for d in CPLX_CLASS for o in OPS_CPLX]
+         + [(d, o) for d in INT_CLASS for o in OPS_INT])
+
+
+def to_dev(torch, arr, offset_bytes=0):
+    """Upload the bytes of `arr` into a fresh device buffer at `offset_bytes`."""
+    raw = np.frombuffer(arr.tobytes(), dtype=np.uint8)
+    buf = torch.zeros(raw.size + offset_bytes + 64, dtype=torch.uint8, device="cuda")
+    buf[offset_bytes:offset_bytes + raw.size] = torch.from_numpy(raw.copy()).cuda()
+    return buf, buf.data_ptr() + offset_bytes
+
+
+def from_dev(buf, offset_bytes, like):
+    raw = buf.cpu().numpy()[offset_bytes:offset_bytes + like.nbytes]
+    return np.frombuffer(raw.tobytes(), dtype=like.dtype).copy()
+
+
+def special_fp(np_t, n, rng):
+    """Random values sprinkled with NaN, +-0, +-inf and denormals."""
+    info = np.finfo(np_t)
+    base = rng.uniform(-2, 2, n).astype(np_t)
+    specials = np.array([np.nan, -np.nan, 0.0, -0.0, np.inf, -np.inf, info.tiny / 4,
+                         -info.tiny / 8, info.max, -info.max, 1.0, -1.0], dtype=np_t)
+    idx = rng.random(n) < 0.3
+    base[idx] = rng.choice(specials, idx.sum())
+    return base
+
+
+def make_inputs(oracle, dt, op, n, rng, special):
+    np_t = oracle.np_type(dt)
+    if special and dt in (23, 24):
+        return special_fp(np_t, n, rng), special_fp(np_t, n, rng)
+    if special and dt in (26, 27):
+        ft = np.float32 if dt == 26 else np.float64
+        def c():
+            re, im = special_fp(ft, n, rng), special_fp(ft, n, rng)
+            return np.stack([re, im], 1).reshape(-1).view(np_t)
+        return c(), c()
+    dist = 1 if op == 6 else 0
+    seed = int(rng.integers(1 << 62))
+    return oracle.fill(dt, dist, seed, 0, n), oracle.fill(dt, dist, seed, 1, n)
+
+
+def same_bits(a, b):
+    return np.array_equal(np.frombuffer(a.tobytes(), np.uint8), np.frombuffer(b.tobytes(), np.uint8))
+
+
+def same_bits_nan_equiv(a, b):
+    """Bitwise equal, except that two NaNs compare equal whatever their payload/sign.
+
+    Used for complex PROD only: which input NaN a NaN product carries depends on the
+    operand order gcc's register allocator and libgcc's __mulsc3 chose on x86; every
+    non-NaN result (including Annex G recovered infinities) is still bit-exact."""
+    ft = np.float32 if a.dtype == np.complex64 else np.float64
+    it = np.uint32 if ft == np.float32 else np.uint64
+    x, y = a.view(ft), b.view(ft)
+    eq = x.view(it) == y.view(it)
+    return bool(np.all(eq | (np.isnan(x) & np.isnan(y))))
+
+
+def check(dt, op, got, ref):
+    if dt in (26, 27) and op == 6:
+        return same_bits_nan_equiv(got, ref)
+    return same_bits(got, ref)
+
+
+@pytest.mark.parametrize("dt,op", PAIRS)
+def test_combine_all_types_ops(torch_cuda, sos, oracle, dt, op):
+    torch = torch_cuda
+    rng = np.random.default_rng(1000 + 17 * dt + op)
+    for n, off in ((1, 0), (7, 0), (4097, 0), (65536 + 3, 0), (1000, 16), (3001, 8)):
+        es = oracle.lib().oracle_type_size(dt)
+        off = (off // es) * es  # element-aligned offsets, keeps `in` and `inout` congruent
+        for special in ((False, True) if dt in (23, 24, 26, 27) else (False,)):
+            a, b = make_inputs(oracle, dt, op, n, rng, special)
+            ref = a.copy()
+            oracle.reduce_local(op, dt, b, ref)
+            da, pa = to_dev(torch, a, off)
+            db, pb = to_dev(torch, b, off)
+            sos.combine(op, dt, pa, pb, n)
+            torch.cuda.synchronize()
+            got = from_dev(da, off, a)
+            assert check(dt, op, got, ref), f"dt={dt} op={op} n={n} off={off} special={special}"
+
+
+@pytest.mark.parametrize("dt,op", [(23, 5), (24, 6), (11, 2), (4, 4), (27, 6), (13, 3)])
+def test_combine_relatively_misaligned(torch_cuda, sos, oracle, dt, op):
+    """`in` and `inout` not 16-B congruent: the element-load path."""
+    torch = torch_cuda
+    rng = np.random.default_rng(7)
+    es = oracle.lib().oracle_type_size(dt)
+    n = 5000
+    a, b = make_inputs(oracle, dt, op, n, rng, False)
+    ref = a.copy()
+    oracle.reduce_local(op, dt, b, ref)
+    da, pa = to_dev(torch, a, 0)
+    db, pb = to_dev(torch, b, es if es < 16 else 0)
+    sos.combine(op, dt, pa, pb, n)
+    torch.cuda.synchronize()
+    assert same_bits(from_dev(da, 0, a), ref)
+
+
+def test_combine3_out_of_place(torch_cuda, sos, oracle):
+    torch = torch_cuda
+    n = 100003
+    a = oracle.fill(23, 0, 5, 0, n)
+    b = oracle.fill(23, 0, 5, 1, n)
+    ref = a.copy()
+    oracle.reduce_local(5, 23, b, ref)
+    da, pa = to_dev(torch, a)
+    db, pb = to_dev(torch, b)
+    dout, po = to_dev(torch, np.zeros_like(a))
+    sos.combine3(5, 23, po, pa, pb, n)
+    torch.cuda.synchronize()
+    assert same_bits(from_dev(dout, 0, a), ref)
+    assert same_bits(from_dev(da, 0, a), a)  # inputs untouched
+
+
+def test_complex_annex_g(torch_cuda, sos, oracle):
+    """Both naive parts NaN -> libgcc __mul[sd]c3 recovery (C99 G.5.1)."""
+    torch = torch_cuda
+    inf, nan = np.inf, np.nan
+    pairs = [((inf, 0.0), (0.0, 1.0)), ((inf, inf), (1.0, 0.0)), ((nan, inf), (2.0, 0.0)),
+             ((1e300, 1e300), (1e300, -1e300)), ((inf, nan), (nan, 1.0)), ((0.0, 0.0), (inf, nan)),
+             ((nan, nan), (1.0, 1.0)), ((-inf, 1.0), (nan, nan)), ((1.0, 2.0), (3.0, -4.0))]
+    for dt, ft in ((27, np.float64), (26, np.float32)):
+        a = np.array([x for x, _ in pairs], dtype=ft).reshape(-1).view(oracle.np_type(dt))
+        b = np.array([y for _, y in pairs], dtype=ft).reshape(-1).view(oracle.np_type(dt))
+        ref = a.copy()
+        oracle.reduce_local(6, dt, b, ref)
+        da, pa = to_dev(torch, a)
+        db, pb = to_dev(torch, b)
+        sos.combine(6, dt, pa, pb, a.size)
+        torch.cuda.synchronize()
+        got = from_dev(da, 0, a)
+        assert same_bits_nan_equiv(got, ref), (dt, got, ref)
+        # the recovered (non-NaN) results must be bit-exact
+        ft = np.float32 if dt == 26 else np.float64
+        fin = ~np.isnan(ref.view(ft))
+        assert np.array_equal(got.view(ft)[fin], ref.view(ft)[fin])
+
+
+def test_invalid_type_and_op(sos):
+    lib = sos.lib()
+    assert lib.sosx_combine(5, 0, None, None, 0, None) == -1      # SIGNED_BYTE
+    assert lib.sosx_combine(5, 7, None, None, 0, None) == -1      # FORTRAN_INTEGER
+    assert lib.sosx_combine(0, 23, None, None, 0, None) == -2     # and on float
+    assert lib.sosx_combine(3, 27, None, None, 0, None) == -2     # min on complex
+    assert lib.sosx_combine(2, 1, None, None, 0, None) == -2      # xor on char (FP class)
+
+
+@pytest.mark.parametrize("dt,op", [(23, 5), (24, 6), (11, 2), (10, 3), (4, 4), (27, 6), (26, 5),
+                                   (9, 5), (13, 0)])
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+def test_fold_matches_oracle_schedules(torch_cuda, sos, oracle, dt, op, P):
+    """LINEAR fold == SOS ring fold order; TREE fold == SOS recdbl_sw result."""
+    torch = torch_cuda
+    n = 3 * 4096 + 5
+    dist = 1 if op == 6 else 0
+    srcs = [oracle.fill(dt, dist, 99, p, n) for p in range(P)]
+    # ring order for a chunk starting at PE c: ((s_c OP s_c+1) OP ...) -> c = 0 here
+    lin = srcs[0].copy()
+    for p in range(1, P):
+        oracle.reduce_local(op, dt, srcs[p], lin)
+    tree = oracle.recdbl(op, dt, srcs)[0]
+    devs = [to_dev(torch, s) for s in srcs]
+    ptrs = [p for _, p in devs]
+    for order, ref in ((0, lin), (1, tree)):
+        dout, po = to_dev(torch, np.zeros_like(srcs[0]))
+        sos.fold(op, dt, order, po, ptrs, n)
+        torch.cuda.synchronize()
+        assert same_bits(from_dev(dout, 0, srcs[0]), ref), f"order={order}"
+
+
+def test_fill_matches_oracle(torch_cuda, sos, oracle):
+    torch = torch_cuda
+    for dt in (23, 24, 26, 27, 4, 11, 13, 9):
+        for dist in (0, 1):
+            n = 10007
+            ref = oracle.fill(dt, dist, 1234, 3, n, 77)
+            buf = torch.zeros(ref.nbytes, dtype=torch.uint8, device="cuda")
+            sos.fill(dt, dist, 1234, 3, buf.data_ptr(), n, 77)
+            torch.cuda.synchronize()
+            assert same_bits(from_dev(buf, 0, ref), ref), (dt, dist)

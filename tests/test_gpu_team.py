@@ -1,0 +1,162 @@
+"""GPU: the team reduction end to end.
+
+* loopback team: P = 1..8 simulated PEs on one MI355X run the exact per-PE plans of
+  the RCCL executor (fused fold kernels, scratch layout, in-place handling) with
+  device-to-device copies as the transport; results must equal the oracle's SOS ring /
+  recdbl bit for bit.
+* public API on one PE: shmem_init + shmem_<T>_<op>_reduce / _to_all on device and
+  host buffers, shmemx_reduce_local, and the example programs.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def dev_bytes(torch, arr, pad=0):
+    raw = np.frombuffer(arr.tobytes(), np.uint8)
+    buf = torch.zeros(raw.size + pad + 64, dtype=torch.uint8, device="cuda")
+    buf[pad:pad + raw.size] = torch.from_numpy(raw.copy()).cuda()
+    return buf
+
+
+def host_view(buf, pad, like):
+    return np.frombuffer(buf.cpu().numpy()[pad:pad + like.nbytes].tobytes(), dtype=like.dtype)
+
+
+CASES = [(23, 5, 0), (24, 6, 1), (11, 2, 0), (4, 4, 0), (18, 3, 0), (27, 6, 1), (26, 5, 0),
+         (1, 5, 0), (10, 0, 0)]
+
+
+@pytest.mark.parametrize("alg", ["ring", "recdbl", "rechalving", "recdbl_direct", "auto"])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 8])
+def test_loopback_schedules(torch_cuda, sos, oracle, alg, P):
+    from sos_amd import shmem as S
+    torch = torch_cuda
+    for dt, op, dist in CASES:
+        if alg in ("rechalving", "recdbl_direct") and (dt, op) in ((4, 4), (18, 3)):
+            continue  # min/max ties are perspective dependent: recdbl/ring only
+        for n in (1, 37, 4096 * 3 + 5):
+            for in_place in (False, True):
+                srcs = [oracle.fill(dt, dist, 500 + n, p, n) for p in range(P)]
+                bytes_ = n * srcs[0].itemsize
+                if alg == "ring" or (alg == "auto" and bytes_ >= 16384):
+                    ref = oracle.ring(op, dt, srcs)
+                else:
+                    ref = oracle.recdbl(op, dt, srcs)
+                pad = 16 * (P % 3)  # some PEs' buffers start off 256-B alignment
+                sb = [dev_bytes(torch, s, pad) for s in srcs]
+                db = sb if in_place else [torch.zeros_like(b) for b in sb]
+                S.loopback_allreduce(alg, op, dt, [b.data_ptr() + pad for b in sb],
+                                     [b.data_ptr() + pad for b in db], n)
+                torch.cuda.synchronize()
+                for p in range(P):
+                    want = ref[p] if alg in ("ring", "recdbl", "auto") else ref[0]
+                    got = host_view(db[p], pad, srcs[p])
+                    assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), \
+                        (alg, P, dt, op, n, in_place, p)
+
+
+def test_loopback_large_ring_fp32(torch_cuda, sos, oracle):
+    """8 PEs x 4Mi fp32 through the ring plan: bit-exact with SOS ring."""
+    from sos_amd import shmem as S
+    torch = torch_cuda
+    P, n = 8, 4 << 20
+    srcs = [oracle.fill(23, 0, 0x5EED, p, n) for p in range(P)]
+    ref = oracle.ring(5, 23, srcs)
+    sb = [torch.from_numpy(s).cuda() for s in srcs]
+    db = [torch.empty_like(b) for b in sb]
+    S.loopback_allreduce("ring", 5, 23, [b.data_ptr() for b in sb], [b.data_ptr() for b in db], n)
+    torch.cuda.synchronize()
+    for p in range(P):
+        assert np.array_equal(db[p].cpu().numpy().view(np.uint32), ref[p].view(np.uint32))
+
+
+@pytest.fixture(scope="module")
+def shmem1(torch_cuda, sos):
+    from sos_amd import shmem as S
+    os.environ.pop("WORLD_SIZE", None)
+    S.shmem_init()
+    assert S.shmem_n_pes() == 1 and S.shmem_my_pe() == 0
+    yield S
+
+
+def test_api_one_pe_device_and_host(torch_cuda, shmem1, oracle):
+    S, torch = shmem1, torch_cuda
+    team = S.team_world()
+    n = 1 << 16
+    src = torch.from_numpy(oracle.fill(23, 0, 1, 0, n)).cuda()
+    dst = torch.zeros_like(src)
+    assert S.shmem_float_sum_reduce(team, dst.data_ptr(), src.data_ptr(), n) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src)  # PE_size 1: copy, as SOS (src/collectives.c:664-668)
+    h = oracle.fill(11, 0, 2, 0, n)
+    out = np.zeros_like(h)
+    assert S.shmem_int64_xor_reduce(team, out.ctypes.data, h.ctypes.data, n) == 0
+    assert np.array_equal(out, h)
+    ld = np.arange(8, dtype=np.longdouble)
+    lo = np.zeros_like(ld)
+    S.shmem_longdouble_sum_reduce(team, lo.ctypes.data, ld.ctypes.data, 8)  # 1 PE: copy works
+    assert np.array_equal(lo, ld)
+
+
+def test_api_to_all_psync_untouched(torch_cuda, shmem1, oracle):
+    S = shmem1
+    n = 1000
+    src = oracle.fill(24, 0, 3, 0, n)
+    dst = np.zeros_like(src)
+    psync = np.zeros(35, dtype=np.int64)
+    pwrk = np.zeros(n // 2 + 1, dtype=np.float64)
+    S.shmem_double_sum_to_all(dst.ctypes.data, src.ctypes.data, n, 0, 0, 1, pwrk.ctypes.data,
+                              psync.ctypes.data)
+    assert np.array_equal(dst, src) and not psync.any()
+
+
+def test_reduce_local_extension(torch_cuda, shmem1, oracle):
+    S, torch = shmem1, torch_cuda
+    n = 12345
+    a, b = oracle.fill(24, 1, 4, 0, n), oracle.fill(24, 1, 4, 1, n)
+    ref = a.copy()
+    oracle.reduce_local(6, 24, b, ref)
+    da, db = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    assert S.shmemx_reduce_local(6, 24, n, db.data_ptr(), da.data_ptr()) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(da.cpu().numpy().view(np.uint64), ref.view(np.uint64))
+
+
+def _run(cmd, timeout=120, env=None):
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
+
+
+def test_examples_one_pe():
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "examples")], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stderr
+    r = _run([os.path.join(ROOT, "examples", "pi_reduce_amd")])
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "Pi from 10000 points on 1 PEs: 3.171200"
+    r = _run([os.path.join(ROOT, "examples", "reduce_types")])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "reduce_types: OK" in r.stdout
+
+
+def test_error_aborts_like_sos():
+    code = ("import ctypes, numpy as np\nfrom sos_amd import shmem as S\nS.shmem_init()\n"
+            "a = np.zeros(4, np.int32)\n"
+            "S.shmem_int_sum_to_all(a.ctypes.data, a.ctypes.data, 4, 0, 0, 5, None, None)\n")
+    r = _run(["python", "-c", code], env={"PYTHONPATH": ROOT})
+    assert r.returncode == 1
+    assert "Invalid active set" in r.stderr
+    code2 = ("import numpy as np\nfrom sos_amd import shmem as S\nS.shmem_init()\n"
+             "a = np.zeros(8, np.int32)\n"
+             "S.shmem_int_sum_reduce(S.team_world(), a.ctypes.data + 4, a.ctypes.data, 4)\n")
+    r = _run(["python", "-c", code2], env={"PYTHONPATH": ROOT})
+    assert r.returncode == 1 and "overlaps" in r.stderr
