@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-pmc", action="store_true")
+    p.add_argument("--no-host", action="store_true", help="skip the host-resident leg")
     p.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -144,6 +145,44 @@ def run_combine(args, torch):
     return res
 
 
+def host_resident(args, torch):
+    """The same combine when inout/in start and end in HOST memory (the SOS symmetric
+    heap is host memory): H2D of both operands, the device combine, D2H of inout.
+    Reported beside `value` (never as it): the PCIe-inclusive end-to-end rate."""
+    from sos_amd import _lib as L
+    dt = L.dtype_id(args.dtype)
+    es = L.dtype_size(dt)
+    n = args.n
+    stream = torch.cuda.current_stream()
+    S = stream.cuda_stream
+    out = {}
+    da = torch.empty(n * es, dtype=torch.uint8, device="cuda")
+    db = torch.empty_like(da)
+    for kind in ("pinned", "pageable"):
+        ha = torch.empty(n * es, dtype=torch.uint8, pin_memory=(kind == "pinned"))
+        hb = torch.empty(n * es, dtype=torch.uint8, pin_memory=(kind == "pinned"))
+        ha.fill_(0)
+        hb.fill_(0)
+        reps = 5
+        for r in range(reps + 1):
+            if r == 1:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            da.copy_(ha, non_blocking=True)
+            db.copy_(hb, non_blocking=True)
+            L.combine(args.op, dt, da.data_ptr(), db.data_ptr(), n, S)
+            ha.copy_(da, non_blocking=True)
+            torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        out[f"{kind}_GiBs"] = round(n * es / t / GiB, 3)
+        out[f"{kind}_ms"] = round(t * 1e3, 3)
+        del ha, hb
+    out["bytes_moved_per_call"] = {"H2D": 2 * n * es, "D2H": n * es}
+    out["note"] = ("payload GiB/s of reduce_local on host-resident operands through the GPU: "
+                   "H2D(inout, in) + combine + D2H(inout); PCIe Gen5 x16 = 63 GB/s spec")
+    return out
+
+
 def variants_ab(args, torch, L, launch):
     """Interleaved A/B of every combine variant in one process (guide rule 24)."""
     lib = L.lib()
@@ -170,6 +209,19 @@ def variants_ab(args, torch, L, launch):
         gbs = 3 * args.n * es / (med / 1e3) / 1e9
         log(f"{lib.sosx_combine_variant_name(v).decode():>18} {med:10.4f} {ms[0]:9.4f} {gbs:20.1f}")
     lib.sosx_set_combine_variant(args.variant)
+    # calibration: the runtime's device-to-device copy of the same bytes (2 streams)
+    a = torch.empty(args.n * es, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(20):
+        b.copy_(a)
+    e.record(stream)
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / 20
+    log(f"{'calib: D2D copy':>18} {ms:10.4f} {'':9} {2 * args.n * es / (ms / 1e3) / 1e9:20.1f}")
 
 
 # ----------------------------------------------------------------------------------
@@ -263,6 +315,8 @@ def main():
                                                "rocprofv3 --pmc, gfx950 FETCH_SIZE halving corrected")
         else:
             res["roofline"]["traffic_note"] = str(info)
+    if rank == 0 and not args.no_host:
+        res["host_resident"] = host_resident(args, torch)
     if rank == 0 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(res), flush=True)

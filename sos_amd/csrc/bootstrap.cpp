@@ -235,3 +235,30 @@ int exchange(int rank, int size, const void *root_blob, size_t root_len, void *o
 }
 
 }  // namespace sosboot
+
+// Test hook (CPU, no GPU): discover rank/size from the launcher environment and run
+// one bootstrap exchange in which PE 0 broadcasts a token and every PE contributes its
+// rank; `all_ranks` (size ints) receives the gathered ranks.  Returns 0 on success.
+extern "C" int sosx_bootstrap_probe(int *rank, int *size, int *all_ranks, int cap,
+                                    unsigned long long *token)
+{
+    int r, s;
+    sosboot::discover(&r, &s);
+    if (rank) *rank = r;
+    if (size) *size = s;
+    if (!all_ranks || cap < s) return -3;
+    unsigned long long tok = 0x5EED0000ull + (unsigned long long)s;
+    unsigned long long got = 0;
+    char err[256] = {0};
+    int32_t me = r;
+    std::vector<int32_t> recs((size_t)s);
+    int rc = sosboot::exchange(r, s, &tok, sizeof(tok), &got, &me, sizeof(me), recs.data(), err,
+                               sizeof(err));
+    if (rc) {
+        fprintf(stderr, "bootstrap probe: %s\n", err);
+        return rc;
+    }
+    for (int i = 0; i < s; ++i) all_ranks[i] = recs[(size_t)i];
+    if (token) *token = got;
+    return 0;
+}

@@ -384,6 +384,10 @@ int sosx_loopback_allreduce(int alg, int P, int op, int datatype, void *const *s
         }
     }
     hipError_t e = hipStreamSynchronize(sm);
+    if (g_prof.on) {
+        g_prof.ncall++;
+        g_prof.collect();
+    }
     for (auto v : scr)
         if (v) (void)hipFree(v);
     return e == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;

@@ -1,0 +1,76 @@
+"""Team-reduction kernels at the headline size on ONE GPU (loopback transport).
+
+P simulated PEs, nreduce elements each, all resident in one MI355X's HBM; runs the
+exact per-PE plans of the RCCL executor with device-to-device copies standing in for
+xGMI.  Reports the fused fold kernel's HBM rate (HIP events via sosx_prof_*) and the
+bit-exactness of the result against an on-GPU schedule-order re-evaluation.
+Run under `rocprofv3 --kernel-trace --stats` for the per-kernel summary.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--P", type=int, default=8)
+    ap.add_argument("--n", type=int, default=128 << 20)
+    ap.add_argument("--alg", default="ring")
+    ap.add_argument("--dtype", default="float")
+    ap.add_argument("--op", default="sum")
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    import torch
+    from sos_amd import _lib as L
+    from sos_amd import shmem as S
+    torch.cuda.set_device(0)
+    dt, op = L.dtype_id(a.dtype), L.op_id(a.op)
+    es = L.dtype_size(dt)
+    dist = L.DIST_PROD if a.op == "prod" else L.DIST_UNIFORM
+    srcs = [torch.empty(a.n * es, dtype=torch.uint8, device="cuda") for _ in range(a.P)]
+    dsts = [torch.empty(a.n * es, dtype=torch.uint8, device="cuda") for _ in range(a.P)]
+    for p, b in enumerate(srcs):
+        L.fill(dt, dist, 0x5EED, p, b.data_ptr(), a.n)
+    torch.cuda.synchronize()
+    sp, dp = [b.data_ptr() for b in srcs], [b.data_ptr() for b in dsts]
+    S.loopback_allreduce(a.alg, op, dt, sp, dp, a.n)  # warm-up
+    S.prof_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        S.loopback_allreduce(a.alg, op, dt, sp, dp, a.n)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    prof = S.prof_get()
+    S.prof_enable(False)
+    # check PE 0 against a direct schedule-order fold
+    exp = torch.empty_like(dsts[0])
+    if a.alg == "ring":
+        q, r = divmod(a.n, a.P)
+        for c in range(a.P):
+            cnt = q + (c < r)
+            first = c * cnt if c < r else c * cnt + r
+            L.fold(op, dt, L.ORDER_LINEAR, exp.data_ptr() + first * es,
+                   [sp[(c + k) % a.P] + first * es for k in range(a.P)], cnt)
+    else:
+        L.fold(op, dt, L.ORDER_TREE, exp.data_ptr(), sp, a.n)
+    torch.cuda.synchronize()
+    bad = L.count_mismatch(exp.data_ptr(), dp[0], a.n, es)
+    nf = max(prof["nfold"], 1)
+    fold_ms = prof["fold_ms"] / nf
+    chunk = a.n // a.P
+    fold_bytes = (a.P + 1) * chunk * es if a.alg in ("ring", "recdbl_direct") else 3 * (a.n // 2) * es
+    out = {"P": a.P, "n": a.n, "alg": a.alg, "fold_launches": prof["nfold"],
+           "fold_mean_ms": round(fold_ms, 5),
+           "fold_GBs": round(fold_bytes / (fold_ms / 1e3) / 1e9, 1),
+           "fold_frac_of_8TBs": round(fold_bytes / (fold_ms / 1e3) / 1e9 / 8000.0, 4),
+           "wall_ms_per_allreduce_all_PEs": round((t1 - t0) / a.iters * 1e3, 3),
+           "mismatches_pe0": bad}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
