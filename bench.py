@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--n", type=int, default=128 << 20, help="nreduce (elements)")
+    p.add_argument("--nreduce", type=int, default=128 << 20, help="nreduce (elements per PE)")
     p.add_argument("--dtype", default="float")
     p.add_argument("--op", default="sum")
     p.add_argument("--alg", default=os.environ.get("SHMEM_REDUCE_ALGORITHM", "auto"))
@@ -56,8 +56,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-host", action="store_true", help="skip the host-resident leg")
+    p.add_argument("--team", action="store_true",
+                   help="run the team (shmem_*_reduce) leg even at WORLD_SIZE 1")
     p.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
-    return p.parse_args()
+    a = p.parse_args()
+    a.n = a.nreduce
+    return a
 
 
 def log(*a):
@@ -240,7 +244,7 @@ def pmc_traffic(args):
         d = tempfile.mkdtemp(prefix="sos_pmc_")
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--child-pmc", "--steps", "3",
-               "--warmup", "1", "--n", str(args.n), "--dtype", args.dtype, "--op", args.op,
+               "--warmup", "1", "--nreduce", str(args.n), "--dtype", args.dtype, "--op", args.op,
                "--variant", str(args.variant)]
         try:
             subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL,
@@ -300,7 +304,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus and not args.child_pmc:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    if world > 1:
+    if world > 1 or args.team:
         from sos_amd import team_bench
         return team_bench.main(args, torch)
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))

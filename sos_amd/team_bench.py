@@ -32,7 +32,7 @@ def main(args, torch):
 
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
-    local = int(os.environ.get("LOCAL_RANK", rank))
+    local = int(os.environ.get("LOCAL_RANK", rank)) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dist.init_process_group("gloo")
     uid = [S.get_unique_id() if rank == 0 else None]
