@@ -123,6 +123,13 @@ int sosx_fill(int dtype, int dist, uint64_t seed, int pe, void *dst, size_t coun
 int sosx_count_mismatch(const void *a, const void *b, size_t count, size_t elem_size,
                         unsigned long long *mismatches, void *stream);
 
+/* Synchronous copy between any host/device addresses (hipMemcpyDefault semantics). */
+int sosx_memcpy(void *dst, const void *src, size_t bytes, void *stream);
+
+/* Multi-segment copy in one launch (peer-to-peer transport gathers). */
+int sosx_gather(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,
+                void *stream);
+
 /* Kernel variant selection for the hot fp32/generic combine (bench/tuning only):
  * returns the previous variant.  0 = default. */
 int sosx_set_combine_variant(int variant);

@@ -183,6 +183,38 @@ void op_to_all(void *target, const void *source, size_t count, size_t ts, const 
     if ((alg == SOSX_ALG_RING || alg == SOSX_ALG_RECDBL_DIRECT) && t.size > SOSX_MAX_FOLD)
         alg = SOSX_ALG_RECHALVING;
 
+    if (s.transport == TRANSPORT_P2P) {
+        // buffers must live in the IPC-mapped device heap; anything else is staged
+        // through this PE's stage region (in place), whose offset is published
+        const char *hb = s.sym_stage;
+        auto in_heap = [&](const void *p) {
+            return hb && (const char *)p >= hb && (const char *)p + bytes <= hb + s.dev_heap_bytes;
+        };
+        const bool direct = in_heap(source) && in_heap(target);
+        const char *dsrc = (const char *)source;
+        char *ddst = (char *)target;
+        if (!direct) {
+            if (bytes > s.sym_stage_bytes)
+                raise_error("%s: %zu bytes outside the device symmetric heap exceed the p2p stage "
+                            "region (SHMEMX_STAGE_BYTES=%zu); allocate with shmemx_malloc_device",
+                            fn, bytes, s.sym_stage_bytes);
+            hip_check(hipMemcpyAsync(s.sym_stage, source, bytes, hipMemcpyDefault, s.stream), "stage in");
+            dsrc = ddst = s.sym_stage;
+        }
+        const Plan &p = cached_plan(alg, t.size, t.my_idx, count, ts, (unsigned)((uintptr_t)dsrc & 15),
+                                    (unsigned)((uintptr_t)ddst & 15));
+        P2PBufs pb{dsrc, ddst, p.scratch_bytes ? (char *)scratch(p.scratch_bytes) : nullptr,
+                   (size_t)(dsrc - hb), (size_t)(ddst - hb)};
+        if (g_prof.on) g_prof.ncall++;
+        rc = p2p_exec(p, t, alg, count, ts, pb, op, dt, s.stream);
+        if (rc) raise_error("%s: %s", fn, status_text(rc));
+        if (!direct)
+            hip_check(hipMemcpyAsync(target, s.sym_stage, bytes, hipMemcpyDefault, s.stream), "stage out");
+        hip_check(hipStreamSynchronize(s.stream), fn);
+        if (g_prof.on) g_prof.collect();
+        return;
+    }
+
     // residency: device pointers run in place; host memory is staged through HBM
     const bool dev_src = is_device_ptr(source);
     const bool dev_dst = target == source ? dev_src : is_device_ptr(target);

@@ -7,6 +7,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <strings.h>
+#include <sys/mman.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <string>
@@ -139,6 +141,13 @@ static void read_env(State &s)
     s.heap_on_device = h && *h && strcmp(h, "0");
     const char *c = getenv("SHMEMX_CHECK_SYMMETRIC");
     s.error_checking = c && *c && strcmp(c, "0");
+    const char *t = getenv("SHMEMX_TRANSPORT");
+    s.transport = (t && !strcmp(t, "p2p")) ? TRANSPORT_P2P : TRANSPORT_RCCL;
+    if (t && strcmp(t, "p2p") && strcmp(t, "rccl")) warn("Ignoring bad SHMEMX_TRANSPORT '%s'", t);
+    s.dev_heap_bytes = atol_scaled(getenv("SHMEMX_DEVICE_HEAP_SIZE"), 2ull << 30);
+    s.sym_stage_bytes = atol_scaled(getenv("SHMEMX_STAGE_BYTES"), 512ull << 20);
+    s.sym_stage_bytes = (s.sym_stage_bytes + 4095) & ~(size_t)4095;
+    if (s.sym_stage_bytes >= s.dev_heap_bytes) s.dev_heap_bytes = s.sym_stage_bytes + (256u << 20);
 }
 
 // ---------------------------------------------------------------------------------
@@ -208,12 +217,42 @@ static void ensure_host_heap(State &s)
     s.host_heap.init((char *)p, s.symmetric_size, false, false);
 }
 
-static void ensure_device_heap(State &s)
+// Collective: every PE creates its device heap [stage | allocations]; when the
+// peer-to-peer transport is on, the heaps are IPC-exported and every PE maps every
+// other PE's heap (xGMI peer memory on the 8-GPU node; the same device in tests).
+void ensure_device_heap()
 {
+    State &s = st();
     if (s.dev_heap.base) return;
-    void *p = nullptr;
-    hip_check(hipMalloc(&p, s.symmetric_size), "hipMalloc(device heap)");
-    s.dev_heap.init((char *)p, s.symmetric_size, true, false);
+    char *base = nullptr;
+    if (s.ext_base) {
+        base = (char *)s.ext_base;
+        s.dev_heap_bytes = s.ext_size;
+        if (s.sym_stage_bytes >= s.ext_size) s.sym_stage_bytes = s.ext_size / 2;
+    } else {
+        hip_check(hipMalloc((void **)&base, s.dev_heap_bytes), "hipMalloc(device heap)");
+    }
+    s.sym_stage = base;
+    s.dev_heap.init(base + s.sym_stage_bytes, s.dev_heap_bytes - s.sym_stage_bytes, true,
+                    s.ext_base != nullptr);
+    s.peer_heap.assign((size_t)s.n_pes, nullptr);
+    s.peer_heap[(size_t)s.my_pe] = base;
+    if (s.transport != TRANSPORT_P2P || s.n_pes == 1) return;
+    if (!s.hub.up) raise_error("SHMEMX_TRANSPORT=p2p needs the shmem_init bootstrap");
+    hipIpcMemHandle_t mine;
+    hip_check(hipIpcGetMemHandle(&mine, base), "hipIpcGetMemHandle(device heap)");
+    std::vector<hipIpcMemHandle_t> all((size_t)s.n_pes);
+    if (sosboot::hub_allgather(&s.hub, &mine, sizeof(mine), all.data()) != 0)
+        raise_error("device heap: IPC handle exchange failed");
+    for (int q = 0; q < s.n_pes; ++q) {
+        if (q == s.my_pe) continue;
+        void *p = nullptr;
+        hip_check(hipIpcOpenMemHandle(&p, all[(size_t)q], hipIpcMemLazyEnablePeerAccess),
+                  "hipIpcOpenMemHandle(peer device heap)");
+        s.peer_heap[(size_t)q] = (char *)p;
+    }
+    debug_msg("device heap %zu B (stage %zu B) mapped on %d PEs", s.dev_heap_bytes,
+              s.sym_stage_bytes, s.n_pes);
 }
 
 // ---------------------------------------------------------------------------------
@@ -271,6 +310,15 @@ bool is_symmetric(const void *p, size_t bytes)
 void team_barrier(const Team &t)
 {
     State &s = st();
+    if (s.shm.base) {
+        // node-local: the stream first (SOS barrier also completes outstanding work),
+        // then the shared-memory arrival counters of this member set
+        hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize(barrier)");
+        if (t.size > 1 && t.my_idx >= 0 && !s.shm.wait(t.start, t.stride, t.size, 600.0))
+            raise_error("barrier timed out (team start %d stride %d size %d)", t.start, t.stride,
+                        t.size);
+        return;
+    }
     if (t.size > 1 && t.my_idx >= 0) {
         for (int d = 1; d < t.size; d <<= 1) {
             const int to = t.world_rank((t.my_idx + d) % t.size);
@@ -289,10 +337,9 @@ Team *team_from_handle(void *handle) { return (Team *)handle; }
 // ---------------------------------------------------------------------------------
 // init (src/init.c:221-567, condensed to what the reduction path needs)
 // ---------------------------------------------------------------------------------
-static void init_common(int pe, int npes, const ncclUniqueId &uid)
+static void init_common(int pe, int npes, const ncclUniqueId *uid)
 {
     State &s = st();
-    read_env(s);
     s.my_pe = pe;
     s.n_pes = npes;
     int ndev = 0;
@@ -305,8 +352,7 @@ static void init_common(int pe, int npes, const ncclUniqueId &uid)
     s.stream = s.own_stream;
     hip_check(hipMalloc((void **)&s.dbar, 64), "hipMalloc(barrier word)");
     hip_check(hipMemset(s.dbar, 0, 64), "hipMemset");
-    nccl_check(ncclCommInitRank(&s.comm, npes, uid, pe), "ncclCommInitRank");
-    if (s.ext_base) s.dev_heap.init((char *)s.ext_base, s.ext_size, true, true);
+    if (uid) nccl_check(ncclCommInitRank(&s.comm, npes, *uid, pe), "ncclCommInitRank");
     s.world = Team();
     s.world.start = 0;
     s.world.stride = 1;
@@ -319,8 +365,10 @@ static void init_common(int pe, int npes, const ncclUniqueId &uid)
     SHMEM_TEAM_SHARED = &s.shared;
     s.initialized = true;
     s.finalized = false;
-    debug_msg("PE %d of %d on device %d, reduce algorithm %d, crossover %zu", pe, npes, s.device,
-              s.reduce_alg, s.coll_size_crossover);
+    if (s.transport == TRANSPORT_P2P || s.ext_base) ensure_device_heap();
+    debug_msg("PE %d of %d on device %d, transport %s, reduce algorithm %d, crossover %zu", pe,
+              npes, s.device, s.transport == TRANSPORT_P2P ? "p2p" : "rccl", s.reduce_alg,
+              s.coll_size_crossover);
     team_barrier(s.world);
 }
 
@@ -334,24 +382,50 @@ void shmem_init(void)
 {
     State &s = st();
     if (s.initialized) return;
+    read_env(s);
     int rank, size;
     sosboot::discover(&rank, &size);
-    ncclUniqueId uid;
-    memset(&uid, 0, sizeof(uid));
-    if (rank == 0) nccl_check(ncclGetUniqueId(&uid), "ncclGetUniqueId");
-    char host[64] = {0}, err[256] = {0};
+    s.my_pe = rank;
+    char err[256] = {0};
+    if (sosboot::hub_connect(&s.hub, rank, size, err, sizeof(err)) != 0)
+        raise_error("shmem_init: %s", err);
+    // PE 0 decides the transport, creates the RCCL id and names the shm segment
+    struct Blob {
+        ncclUniqueId uid;
+        char shm_name[64];
+        int transport;
+    } blob;
+    memset(&blob, 0, sizeof(blob));
+    if (rank == 0) {
+        blob.transport = s.transport;
+        if (blob.transport == TRANSPORT_RCCL) nccl_check(ncclGetUniqueId(&blob.uid), "ncclGetUniqueId");
+        snprintf(blob.shm_name, sizeof(blob.shm_name), "/sosx_%d_%lx", (int)getpid(),
+                 (unsigned long)time(nullptr));
+    }
+    if (sosboot::hub_bcast(&s.hub, &blob, sizeof(blob)) != 0) raise_error("shmem_init: bootstrap broadcast failed");
+    s.transport = blob.transport;
+    char host[64] = {0};
     gethostname(host, sizeof(host) - 1);
     std::string recs((size_t)size * sizeof(host), '\0');
-    if (sosboot::exchange(rank, size, &uid, sizeof(uid), &uid, host, sizeof(host), &recs[0], err,
-                          sizeof(err)) != 0) {
-        s.my_pe = rank;
-        raise_error("shmem_init: %s", err);
-    }
+    if (sosboot::hub_allgather(&s.hub, host, sizeof(host), &recs[0]) != 0)
+        raise_error("shmem_init: bootstrap all-gather failed");
     for (int r = 0; r < size; ++r)
         if (strncmp(&recs[(size_t)r * sizeof(host)], host, sizeof(host)) != 0)
             raise_error("shmem_init: PE %d runs on another node; this build is single-node "
                         "(one PE per MI355X over xGMI)", r);
-    init_common(rank, size, uid);
+    if (size > 1) {
+        // node-local shared memory: barriers + peer-to-peer transport counters
+        int dummy = 0;
+        std::vector<int> all((size_t)size);
+        if (rank == 0 && !s.shm.attach(blob.shm_name, true, rank, p2p_shared_bytes()))
+            raise_error("shmem_init: cannot create shared memory %s", blob.shm_name);
+        sosboot::hub_allgather(&s.hub, &dummy, sizeof(dummy), all.data());
+        if (rank != 0 && !s.shm.attach(blob.shm_name, false, rank, p2p_shared_bytes()))
+            raise_error("shmem_init: cannot attach shared memory %s", blob.shm_name);
+        sosboot::hub_allgather(&s.hub, &dummy, sizeof(dummy), all.data());
+        if (rank == 0) shm_unlink(blob.shm_name);
+    }
+    init_common(rank, size, s.transport == TRANSPORT_RCCL ? &blob.uid : nullptr);
 }
 
 int shmem_init_thread(int requested, int *provided)
@@ -384,7 +458,14 @@ int shmemx_init_attr(int my_pe, int n_pes, const void *uid, size_t len)
         return SOSX_ERR_ARG;
     ncclUniqueId id;
     memcpy(&id, uid, sizeof(id));
-    init_common(my_pe, n_pes, id);
+    State &s = st();
+    read_env(s);
+    s.my_pe = my_pe;
+    if (s.transport == TRANSPORT_P2P) {
+        warn("SHMEMX_TRANSPORT=p2p needs the shmem_init bootstrap; using RCCL");
+        s.transport = TRANSPORT_RCCL;
+    }
+    init_common(my_pe, n_pes, &id);
     return SOSX_OK;
 }
 
@@ -402,9 +483,15 @@ void shmem_finalize(void)
     s.scratch_bytes = s.stage_bytes = 0;
     s.dbar = nullptr;
     if (s.host_heap.base) (void)hipHostFree(s.host_heap.base);
-    if (s.dev_heap.base && !s.dev_heap.external) (void)hipFree(s.dev_heap.base);
+    for (size_t q = 0; q < s.peer_heap.size(); ++q)
+        if ((int)q != s.my_pe && s.peer_heap[q]) (void)hipIpcCloseMemHandle(s.peer_heap[q]);
+    s.peer_heap.clear();
+    if (s.sym_stage && !s.dev_heap.external) (void)hipFree(s.sym_stage);
+    s.sym_stage = nullptr;
     s.host_heap = Heap();
     s.dev_heap = Heap();
+    s.shm.detach();
+    sosboot::hub_close(&s.hub);
     for (auto &kv : s.dev_allocs) (void)hipFree(kv.first);
     s.dev_allocs.clear();
     if (s.own_stream) (void)hipStreamDestroy(s.own_stream);
@@ -453,7 +540,7 @@ void *shmem_malloc(size_t size)
     {
         std::lock_guard<std::mutex> g(s.mu);
         if (s.heap_on_device) {
-            ensure_device_heap(s);
+            ensure_device_heap();
             p = s.dev_heap.alloc(size, 256);
         } else {
             ensure_host_heap(s);
@@ -488,7 +575,7 @@ void *shmem_align(size_t alignment, size_t size)
     {
         std::lock_guard<std::mutex> g(s.mu);
         Heap &h = s.heap_on_device ? s.dev_heap : s.host_heap;
-        if (s.heap_on_device) ensure_device_heap(s); else ensure_host_heap(s);
+        if (s.heap_on_device) ensure_device_heap(); else ensure_host_heap(s);
         p = h.alloc(size, alignment);
     }
     team_barrier(s.world);
@@ -536,11 +623,14 @@ void *shmemx_malloc_device(size_t size)
     check_initialized("shmemx_malloc_device");
     State &s = st();
     void *p = nullptr;
-    hip_check(hipMalloc(&p, size ? size : 1), "hipMalloc(shmemx_malloc_device)");
+    ensure_device_heap();  // collective, like the call itself
     {
         std::lock_guard<std::mutex> g(s.mu);
-        s.dev_allocs[p] = size;
+        p = s.dev_heap.alloc(size, 256);
     }
+    if (!p && size)
+        raise_error("shmemx_malloc_device(%zu): device heap exhausted (SHMEMX_DEVICE_HEAP_SIZE=%zu)",
+                    size, s.dev_heap_bytes);
     team_barrier(s.world);
     return p;
 }
@@ -551,10 +641,8 @@ void shmemx_free_device(void *ptr)
     State &s = st();
     team_barrier(s.world);
     std::lock_guard<std::mutex> g(s.mu);
-    auto it = s.dev_allocs.find(ptr);
-    if (it == s.dev_allocs.end()) raise_error("shmemx_free_device: %p was not allocated by shmemx_malloc_device", ptr);
-    s.dev_allocs.erase(it);
-    hip_check(hipFree(ptr), "hipFree");
+    if (!s.dev_heap.release(ptr))
+        raise_error("shmemx_free_device: %p was not allocated by shmemx_malloc_device", ptr);
 }
 
 void shmemx_heap_create(void *base, size_t size, int device_type, int device_index)

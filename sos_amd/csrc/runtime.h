@@ -23,10 +23,17 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <vector>
 
+#include "bootstrap.h"
 #include "sosx.h"
 
 namespace sosrt {
+
+enum Transport : int {
+    TRANSPORT_RCCL = 0,  // RCCL ncclSend/ncclRecv over xGMI (default, any device buffer)
+    TRANSPORT_P2P = 1,   // kernels read peers' HBM through the IPC-mapped device heap
+};
 
 struct Team {
     int start = 0, stride = 1, size = 1;
@@ -71,6 +78,15 @@ struct State {
     int *dbar = nullptr;              // 1-int device word for barriers
     Heap host_heap;                   // shmem_malloc (pinned host)
     Heap dev_heap;                    // shmemx_malloc_device / external HIP heap
+    // device symmetric heap layout: [stage region | user allocations]
+    size_t dev_heap_bytes = 2ull << 30;
+    size_t sym_stage_bytes = 512ull << 20;
+    char *sym_stage = nullptr;            // reserved at the heap start, same offset on every PE
+    std::vector<char *> peer_heap;        // each PE's heap base as mapped here (IPC)
+    // control plane
+    sosboot::Hub hub;                 // TCP star to PE 0 (shmem_init path)
+    sosboot::ShmBarrier shm;          // node-local barrier + transport counters
+    int transport = TRANSPORT_RCCL;
     std::map<void *, size_t> dev_allocs;  // direct device allocations (no heap)
     // external heap registered before init (shmemx_heap_create)
     void *ext_base = nullptr;
@@ -115,4 +131,24 @@ void team_barrier(const Team &t);
 
 Team *team_from_handle(void *handle);
 
+// The device symmetric heap (created collectively; IPC-exported to every PE when the
+// peer-to-peer transport is on).
+void ensure_device_heap();
+
+// Per-pair transport counters living in the shared-memory segment (p2p.cpp).
+size_t p2p_shared_bytes();
+
+}  // namespace sosrt
+
+// peer-to-peer executor (p2p.cpp)
+namespace sosplan { struct Plan; }
+namespace sosrt {
+struct P2PBufs {
+    const char *src;
+    char *dst;
+    char *scr;
+    size_t src_off, dst_off;  // heap offsets of src/dst (published to the peers)
+};
+int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, uint64_t ts,
+             const P2PBufs &b, int op, int dt, hipStream_t stream);
 }  // namespace sosrt

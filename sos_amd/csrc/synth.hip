@@ -143,6 +143,14 @@ int sosx_fill(int dtype, int dist, uint64_t seed, int pe, void *dst, size_t coun
     return hip_ok(hipGetLastError());
 }
 
+int sosx_memcpy(void *dst, const void *src, size_t bytes, void *stream)
+{
+    hipStream_t st = as_stream(stream);
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return hip_ok(e);
+}
+
 int sosx_count_mismatch(const void *a, const void *b, size_t count, size_t elem_size,
                         unsigned long long *mismatches, void *stream)
 {

@@ -1,0 +1,61 @@
+"""GPU, multiple processes on one MI355X: the peer-to-peer transport end to end.
+
+tools/oshrun starts P PEs (P = 2, 3, 4, 8) on the box's single GPU with
+SHMEMX_TRANSPORT=p2p: each PE maps every other PE's device heap through IPC and the
+plans' transfers become direct reads of peer HBM, synchronised through node shared
+memory -- the same code that reads xGMI peer memory on the 8-GPU node.  (RCCL refuses
+two ranks on one GPU, so the RCCL transport's multi-PE runs are the 8-GPU bench's.)
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OSHRUN = os.path.join(ROOT, "tools", "oshrun")
+
+
+def oshrun(np_, cmd, timeout=600):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update({"SHMEMX_TRANSPORT": "p2p", "SHMEMX_DEVICE_HEAP_SIZE": "256M",
+                "SHMEMX_STAGE_BYTES": "64M", "SHMEMX_DEVICE": "0", "PYTHONPATH": ROOT})
+    return subprocess.run([sys.executable, OSHRUN, "-np", str(np_), "--timeout", str(timeout - 30),
+                           *cmd], capture_output=True, text=True, timeout=timeout, env=env)
+
+
+@pytest.fixture(scope="module")
+def examples():
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "examples")], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stderr
+    return os.path.join(ROOT, "examples")
+
+
+GOLDEN_PI = {2: "Pi from 20000 points on 2 PEs: 3.164400",
+             4: "Pi from 40000 points on 4 PEs: 3.154100",
+             8: "Pi from 80000 points on 8 PEs: 3.150200"}
+
+
+@pytest.mark.parametrize("np_", [2, 4, 8])
+def test_pi_reduce_multi_pe(examples, np_):
+    r = oshrun(np_, [os.path.join(examples, "pi_reduce_amd")], timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("Pi from")]
+    assert lines == [GOLDEN_PI[np_]], r.stdout
+
+
+def test_reduce_types_4_pes(examples):
+    r = oshrun(4, [os.path.join(examples, "reduce_types")], timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert "reduce_types: OK (4 PEs)" in r.stdout
+
+
+@pytest.mark.parametrize("np_", [2, 3, 4, 8])
+def test_team_check(np_):
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900)
+    ok = [ln for ln in r.stdout.splitlines() if "checks OK" in ln]
+    assert r.returncode == 0 and len(ok) == np_, r.stdout + r.stderr[-3000:]

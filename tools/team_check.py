@@ -1,0 +1,151 @@
+"""Multi-PE correctness run of the public reduction API (one process per PE).
+
+Run under tools/oshrun: every PE calls shmem_<T>_<op>_reduce for every schedule
+(auto, ring, recdbl, rechalving, recdbl_direct), several types/ops and sizes, on
+device-heap buffers (shmemx_malloc_device), on plain device buffers and on host
+buffers, in and out of place, over SHMEM_TEAM_WORLD and over a split team.  Each PE
+checks its own result bit for bit against an on-GPU re-evaluation of the schedule's
+element order over all PEs' regenerated inputs.  Prints one line per PE, exit 0 = OK.
+"""
+import ctypes
+import os
+import sys
+import zlib
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from sos_amd import _lib as L  # noqa: E402
+from sos_amd import shmem as S  # noqa: E402
+
+CASES = [("float", "sum"), ("double", "prod"), ("int64", "xor"), ("int", "max"), ("complexd", "prod"),
+         ("short", "sum"), ("uint8", "min"), ("ulong", "or")]
+ALGS = ["auto", "ring", "recdbl", "rechalving", "recdbl_direct"]
+SIZES = [1, 37, 5003, (1 << 20) + 3]
+
+
+def expected(dt, opid, dist, seed, members, my_idx, n, es, alg_resolved, pe_of):
+    P = len(members)
+    ins = []
+    for i in range(P):
+        b = torch.empty(n * es, dtype=torch.uint8, device="cuda")
+        L.fill(dt, dist, seed, pe_of(i), b.data_ptr(), n)
+        ins.append(b)
+    exp = torch.empty(n * es, dtype=torch.uint8, device="cuda")
+    if P == 1:
+        exp.copy_(ins[0])
+    elif alg_resolved == L.ALGS["ring"]:
+        q, r = divmod(n, P)
+        for c in range(P):
+            cnt = q + (c < r)
+            first = c * cnt if c < r else c * cnt + r
+            if cnt:
+                L.fold(opid, dt, L.ORDER_LINEAR, exp.data_ptr() + first * es,
+                       [ins[(c + k) % P].data_ptr() + first * es for k in range(P)], cnt)
+    else:
+        L.fold(opid, dt, L.ORDER_TREE, exp.data_ptr(), [x.data_ptr() for x in ins], n)
+    torch.cuda.synchronize()
+    return exp
+
+
+def main():
+    S.shmem_init()
+    me, P = S.shmem_my_pe(), S.shmem_n_pes()
+    torch.cuda.set_device(S.lib().shmemx_get_device())
+    world = S.team_world()
+    bad = []
+    checks = 0
+    maxn = max(SIZES)
+    hsrc = S.shmemx_malloc_device(maxn * 16)
+    hdst = S.shmemx_malloc_device(maxn * 16)
+    # an even-PE team (split_strided), when there are at least 3 PEs
+    even = ctypes.c_void_p(0)
+    if P >= 3:
+        S.lib().shmem_team_split_strided(world, 0, 2, (P + 1) // 2, None, 0, ctypes.byref(even))
+    for alg in ALGS:
+        S.shmemx_set_reduce_algorithm(L.ALGS[alg])
+        for tname, oname in CASES:
+            # the binding's internal type: SOS reduces uint8..64 as INT8..64
+            # (bindings/shmem_bind_c.m4:113-116, :136-139, :162-165)
+            dt = L.dtype_id({"uint8": "int8", "uint16": "int16", "uint32": "int32",
+                             "uint64": "int64"}.get(tname, tname))
+            opid = L.op_id(oname)
+            es = L.dtype_size(dt)
+            dist = L.DIST_PROD if oname == "prod" else L.DIST_UNIFORM
+            fn = getattr(S, f"shmem_{tname}_{oname}_reduce")
+            for n in SIZES:
+                if n > 5003 and (tname, oname) not in (("float", "sum"), ("int64", "xor")):
+                    continue
+                seed = zlib.crc32(f"{alg}/{tname}/{oname}/{n}".encode())
+                resolved = S.lib().sosx_resolve_alg(L.ALGS[alg], n * es, 16384)
+                for mode in ("heap", "heap_inplace", "device", "host"):
+                    if mode == "host" and n > 5003:
+                        continue
+                    L.fill(dt, dist, seed, me, hsrc, n)
+                    torch.cuda.synchronize()
+                    if mode == "heap":
+                        fn(world, hdst, hsrc, n)
+                        out = hdst
+                    elif mode == "heap_inplace":
+                        fn(world, hsrc, hsrc, n)
+                        out = hsrc
+                    elif mode == "device":
+                        t_in = torch.empty(n * es, dtype=torch.uint8, device="cuda")
+                        t_out = torch.empty_like(t_in)
+                        L.fill(dt, dist, seed, me, t_in.data_ptr(), n)
+                        torch.cuda.synchronize()
+                        fn(world, t_out.data_ptr(), t_in.data_ptr(), n)
+                        out = t_out.data_ptr()
+                    else:
+                        h_in = _download(hsrc, n * es)
+                        h_out = np.zeros_like(h_in)
+                        fn(world, h_out.ctypes.data, h_in.ctypes.data, n)
+                        tmp = torch.from_numpy(h_out).cuda()
+                        torch.cuda.synchronize()
+                        out = tmp.data_ptr()
+                    exp = expected(dt, opid, dist, seed, list(range(P)), me, n, es, resolved, lambda i: i)
+                    mm = L.count_mismatch(exp.data_ptr(), out, n, es)
+                    checks += 1
+                    if mm:
+                        bad.append((alg, tname, oname, n, mode, mm))
+                # split team: even PEs reduce among themselves
+                if even.value and n <= 5003:
+                    L.fill(dt, dist, seed, me, hsrc, n)
+                    torch.cuda.synchronize()
+                    fn(even.value, hdst, hsrc, n)
+                    m = (P + 1) // 2
+                    exp = expected(dt, opid, dist, seed, list(range(m)), me // 2, n, es, resolved,
+                                   lambda i: 2 * i)
+                    mm = L.count_mismatch(exp.data_ptr(), hdst, n, es)
+                    checks += 1
+                    if mm:
+                        bad.append((alg, tname, oname, n, "even_team", mm))
+    S.shmem_barrier_all()
+    S.shmemx_free_device(hdst)
+    S.shmemx_free_device(hsrc)
+    if even.value:
+        S.lib().shmem_team_destroy(even)
+    S.shmem_finalize()
+    if bad:
+        print(f"PE {me}/{P}: {len(bad)} of {checks} checks FAILED: {bad[:6]}", flush=True)
+        return 1
+    print(f"PE {me}/{P}: {checks} checks OK", flush=True)
+    return 0
+
+
+def _download(ptr, nbytes):
+    """Host copy of `nbytes` of device memory at `ptr` (a heap address)."""
+    t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    _hip_copy(t.data_ptr(), ptr, nbytes)
+    return t.cpu().numpy()
+
+
+def _hip_copy(dst, src, nbytes):
+    L.check(L.lib().sosx_memcpy(dst, src, nbytes, None), "sosx_memcpy")
+
+
+if __name__ == "__main__":
+    sys.exit(main())
