@@ -48,6 +48,14 @@ SHMEM_FUNCTION_ATTRIBUTES int shmemx_get_device(void);
 SHMEM_FUNCTION_ATTRIBUTES int shmemx_reduce_local(int op, int datatype, size_t count,
                                                   const void *in, void *inout);
 
+/* Inter-PE transport of the team reductions (SHMEMX_TRANSPORT=rccl|p2p|both at init):
+ * SOSX_TRANSPORT_RCCL = ncclSend/ncclRecv over xGMI (any device buffer);
+ * SOSX_TRANSPORT_P2P  = kernels read peers' HBM through the IPC-mapped device heap.
+ * Returns the previous transport, or -1 if the requested one was not set up. */
+#define SOSX_TRANSPORT_RCCL 0
+#define SOSX_TRANSPORT_P2P  1
+SHMEM_FUNCTION_ATTRIBUTES int shmemx_set_transport(int transport);
+
 /* Reduction algorithm control, as SHMEM_REDUCE_ALGORITHM (src/collectives.c:195-210):
  * SOSX_ALG_AUTO / _RECDBL / _RING / _RECHALVING / _RECDBL_DIRECT. */
 SHMEM_FUNCTION_ATTRIBUTES int shmemx_set_reduce_algorithm(int alg);

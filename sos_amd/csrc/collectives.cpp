@@ -75,6 +75,21 @@ struct Prof {
 };
 Prof g_prof;
 
+}  // namespace
+
+namespace sosrt {
+// phase-timing hooks shared with the peer-to-peer executor (p2p.cpp)
+void prof_mark(int which, bool end, hipStream_t s)
+{
+    if (!g_prof.on) return;
+    auto &v = which == 0 ? g_prof.fold_ev : g_prof.xfer_ev;
+    auto &n = which == 0 ? g_prof.nf : g_prof.nx;
+    (void)hipEventRecord(g_prof.get(v, n, end), s);
+}
+}  // namespace sosrt
+
+namespace {
+
 struct Bufs {
     const char *src;
     char *dst;

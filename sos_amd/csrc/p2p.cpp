@@ -40,6 +40,8 @@ extern "C" int sosx_gather(int nseg, const void *const *srcs, void *const *dsts,
 
 namespace sosrt {
 
+void prof_mark(int which, bool end, hipStream_t s);  // collectives.cpp (0 = fold, 1 = transfer)
+
 namespace {
 
 constexpr int kMaxPE = 64;
@@ -189,7 +191,9 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
                 gb.push_back(sg.bytes);
             }
         if (!gs.empty()) {
+            prof_mark(1, false, stream);
             int rc = sosx_gather((int)gs.size(), gs.data(), gd.data(), gb.data(), stream);
+            prof_mark(1, true, stream);
             if (rc) return rc;
         }
         auto run_ops = [&]() -> int {
@@ -202,8 +206,10 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
                         return SOSX_ERR_HIP;
                     continue;
                 }
+                prof_mark(0, false, stream);
                 int rc = sosx_fold(op, dt, l.order, local_ptr(l.out_buf, l.out_off),
                                    fold_ins[i].data(), l.nin, l.count, stream);
+                prof_mark(0, true, stream);
                 if (rc) return rc;
             }
             return SOSX_OK;

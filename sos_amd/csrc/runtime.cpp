@@ -141,9 +141,14 @@ static void read_env(State &s)
     s.heap_on_device = h && *h && strcmp(h, "0");
     const char *c = getenv("SHMEMX_CHECK_SYMMETRIC");
     s.error_checking = c && *c && strcmp(c, "0");
+    // rccl (default) | p2p | both (RCCL communicator AND IPC-mapped heap; calls use RCCL
+    // until shmemx_set_transport(SOSX_TRANSPORT_P2P))
     const char *t = getenv("SHMEMX_TRANSPORT");
     s.transport = (t && !strcmp(t, "p2p")) ? TRANSPORT_P2P : TRANSPORT_RCCL;
-    if (t && strcmp(t, "p2p") && strcmp(t, "rccl")) warn("Ignoring bad SHMEMX_TRANSPORT '%s'", t);
+    s.want_rccl = !(t && !strcmp(t, "p2p"));
+    s.want_p2p = t && (!strcmp(t, "p2p") || !strcmp(t, "both"));
+    if (t && strcmp(t, "p2p") && strcmp(t, "rccl") && strcmp(t, "both"))
+        warn("Ignoring bad SHMEMX_TRANSPORT '%s'", t);
     s.dev_heap_bytes = atol_scaled(getenv("SHMEMX_DEVICE_HEAP_SIZE"), 2ull << 30);
     s.sym_stage_bytes = atol_scaled(getenv("SHMEMX_STAGE_BYTES"), 512ull << 20);
     s.sym_stage_bytes = (s.sym_stage_bytes + 4095) & ~(size_t)4095;
@@ -237,7 +242,8 @@ void ensure_device_heap()
                     s.ext_base != nullptr);
     s.peer_heap.assign((size_t)s.n_pes, nullptr);
     s.peer_heap[(size_t)s.my_pe] = base;
-    if (s.transport != TRANSPORT_P2P || s.n_pes == 1) return;
+    s.p2p_ready = s.n_pes == 1;
+    if (!s.want_p2p || s.n_pes == 1) return;
     if (!s.hub.up) raise_error("SHMEMX_TRANSPORT=p2p needs the shmem_init bootstrap");
     hipIpcMemHandle_t mine;
     hip_check(hipIpcGetMemHandle(&mine, base), "hipIpcGetMemHandle(device heap)");
@@ -251,6 +257,7 @@ void ensure_device_heap()
                   "hipIpcOpenMemHandle(peer device heap)");
         s.peer_heap[(size_t)q] = (char *)p;
     }
+    s.p2p_ready = true;
     debug_msg("device heap %zu B (stage %zu B) mapped on %d PEs", s.dev_heap_bytes,
               s.sym_stage_bytes, s.n_pes);
 }
@@ -365,7 +372,7 @@ static void init_common(int pe, int npes, const ncclUniqueId *uid)
     SHMEM_TEAM_SHARED = &s.shared;
     s.initialized = true;
     s.finalized = false;
-    if (s.transport == TRANSPORT_P2P || s.ext_base) ensure_device_heap();
+    if (s.want_p2p || s.ext_base) ensure_device_heap();
     debug_msg("PE %d of %d on device %d, transport %s, reduce algorithm %d, crossover %zu", pe,
               npes, s.device, s.transport == TRANSPORT_P2P ? "p2p" : "rccl", s.reduce_alg,
               s.coll_size_crossover);
@@ -393,17 +400,21 @@ void shmem_init(void)
     struct Blob {
         ncclUniqueId uid;
         char shm_name[64];
-        int transport;
+        int transport, want_rccl, want_p2p;
     } blob;
     memset(&blob, 0, sizeof(blob));
     if (rank == 0) {
         blob.transport = s.transport;
-        if (blob.transport == TRANSPORT_RCCL) nccl_check(ncclGetUniqueId(&blob.uid), "ncclGetUniqueId");
+        blob.want_rccl = s.want_rccl;
+        blob.want_p2p = s.want_p2p;
+        if (blob.want_rccl) nccl_check(ncclGetUniqueId(&blob.uid), "ncclGetUniqueId");
         snprintf(blob.shm_name, sizeof(blob.shm_name), "/sosx_%d_%lx", (int)getpid(),
                  (unsigned long)time(nullptr));
     }
     if (sosboot::hub_bcast(&s.hub, &blob, sizeof(blob)) != 0) raise_error("shmem_init: bootstrap broadcast failed");
     s.transport = blob.transport;
+    s.want_rccl = blob.want_rccl;
+    s.want_p2p = blob.want_p2p;
     char host[64] = {0};
     gethostname(host, sizeof(host) - 1);
     std::string recs((size_t)size * sizeof(host), '\0');
@@ -425,7 +436,7 @@ void shmem_init(void)
         sosboot::hub_allgather(&s.hub, &dummy, sizeof(dummy), all.data());
         if (rank == 0) shm_unlink(blob.shm_name);
     }
-    init_common(rank, size, s.transport == TRANSPORT_RCCL ? &blob.uid : nullptr);
+    init_common(rank, size, s.want_rccl ? &blob.uid : nullptr);
 }
 
 int shmem_init_thread(int requested, int *provided)
@@ -461,10 +472,12 @@ int shmemx_init_attr(int my_pe, int n_pes, const void *uid, size_t len)
     State &s = st();
     read_env(s);
     s.my_pe = my_pe;
-    if (s.transport == TRANSPORT_P2P) {
-        warn("SHMEMX_TRANSPORT=p2p needs the shmem_init bootstrap; using RCCL");
+    if (s.want_p2p) {
+        warn("SHMEMX_TRANSPORT=p2p/both needs the shmem_init bootstrap; using RCCL only");
         s.transport = TRANSPORT_RCCL;
+        s.want_p2p = false;
     }
+    s.want_rccl = true;
     init_common(my_pe, n_pes, &id);
     return SOSX_OK;
 }
@@ -670,6 +683,17 @@ void shmemx_set_stream(void *hip_stream)
 void *shmemx_get_stream(void) { return (void *)st().stream; }
 
 int shmemx_get_device(void) { return st().device; }
+
+int shmemx_set_transport(int transport)
+{
+    State &s = st();
+    const int prev = s.transport;
+    if (transport == TRANSPORT_RCCL && s.comm) s.transport = TRANSPORT_RCCL;
+    else if (transport == TRANSPORT_P2P && s.p2p_ready && (s.shm.base || s.n_pes == 1))
+        s.transport = TRANSPORT_P2P;
+    else return -1;
+    return prev;
+}
 
 int shmemx_set_reduce_algorithm(int alg)
 {

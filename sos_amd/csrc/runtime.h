@@ -86,7 +86,10 @@ struct State {
     // control plane
     sosboot::Hub hub;                 // TCP star to PE 0 (shmem_init path)
     sosboot::ShmBarrier shm;          // node-local barrier + transport counters
-    int transport = TRANSPORT_RCCL;
+    int transport = TRANSPORT_RCCL;   // the transport calls use now
+    bool want_rccl = true;            // create the RCCL communicator
+    bool want_p2p = false;            // IPC-map the device heap on every PE
+    bool p2p_ready = false;           // heap mapped (or single PE)
     std::map<void *, size_t> dev_allocs;  // direct device allocations (no heap)
     // external heap registered before init (shmemx_heap_create)
     void *ext_base = nullptr;

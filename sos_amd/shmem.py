@@ -35,6 +35,8 @@ _RUNTIME = {
     "shmemx_set_stream": (None, [_c.c_void_p]),
     "shmemx_get_stream": (_c.c_void_p, []),
     "shmemx_set_reduce_algorithm": (_c.c_int, [_c.c_int]),
+    "shmemx_set_transport": (_c.c_int, [_c.c_int]),
+    "shmemx_get_device": (_c.c_int, []),
     "shmemx_reduce_local": (_c.c_int, [_c.c_int, _c.c_int, _c.c_size_t, _c.c_void_p, _c.c_void_p]),
     "sosx_loopback_allreduce": (_c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                            _c.POINTER(_c.c_void_p), _c.POINTER(_c.c_void_p),

@@ -1,14 +1,19 @@
 """N > 1 leg of bench.py: shmem_<T>_<op>_reduce over one PE per GPU.
 
 Launched by torchrun (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).  torch.distributed
-(gloo, CPU) is only the bench's control plane: it broadcasts the RCCL unique id and
-takes the barrier / max-over-ranks of the timing.  The data path is libsos_amd.so:
-RCCL over xGMI between PEs + the HIP fold kernels, behind the public C API.
+(gloo, CPU) is only the bench's control plane (barrier, max over ranks).  The data path
+is libsos_amd.so behind the public C API: shmem_init() bootstraps over TCP
+(MASTER_ADDR, MASTER_PORT + 1), source/target live in the device symmetric heap
+(shmemx_malloc_device), and every step is one shmem_<T>_<op>_reduce(SHMEM_TEAM_WORLD).
 
-Self-check: after the timed steps every rank regenerates all P inputs on its own GPU
-and evaluates the schedule's element order with the fold kernel (ring: chunk c
-folded from PE c rightwards, src/collectives.c:693-727; tree schedules: the recdbl_sw
-tree), then compares its team result bit for bit.
+Both inter-PE transports are measured (SHMEMX_TRANSPORT=both):
+  rccl : ncclSend/ncclRecv over xGMI + the HIP fold kernels (the library default;
+         `value` is this one)
+  p2p  : the fold kernel reads the peers' chunks straight out of their IPC-mapped HBM.
+Self-check: after timing, every rank regenerates all P inputs on its own GPU and
+re-evaluates the schedule's element order with the fold kernel (ring: chunk c folded
+from PE c rightwards, src/collectives.c:693-727; tree schedules: the recdbl_sw tree),
+then compares its team result bit for bit.
 """
 import json
 import os
@@ -34,67 +39,87 @@ def main(args, torch):
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank)) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
-    dist.init_process_group("gloo")
-    uid = [S.get_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    os.environ.setdefault("SHMEMX_DEVICE", str(local))
-    S.init_attr(rank, world, uid[0])
-    alg = L.ALGS[args.alg]
-    S.shmemx_set_reduce_algorithm(alg)
-
     dt = L.dtype_id(args.dtype)
     es = L.dtype_size(dt)
     n = args.n
+    os.environ.setdefault("SHMEMX_TRANSPORT", "both")
+    os.environ.setdefault("SHMEMX_DEVICE_HEAP_SIZE", str(2 * n * es + (320 << 20)))
+    os.environ.setdefault("SHMEMX_STAGE_BYTES", str(64 << 20))
+    os.environ.setdefault("SHMEMX_DEVICE", str(local))
+    dist.init_process_group("gloo")
+    S.shmem_init()
+    assert S.shmem_n_pes() == world and S.shmem_my_pe() == rank
+    alg = L.ALGS[args.alg]
+    S.shmemx_set_reduce_algorithm(alg)
+
     dist_kind = L.DIST_PROD if args.op == "prod" else L.DIST_UNIFORM
     seed = 0x5EED
     stream = S.lib().shmemx_get_stream()
-    src = torch.empty(n * es, dtype=torch.uint8, device="cuda")
-    dst = torch.empty(n * es, dtype=torch.uint8, device="cuda")
-    L.fill(dt, dist_kind, seed, rank, src.data_ptr(), n, 0, stream)
+    src = S.shmemx_malloc_device(n * es)
+    dst = S.shmemx_malloc_device(n * es)
+    L.fill(dt, dist_kind, seed, rank, src, n, 0, stream)
     torch.cuda.synchronize()
     fn = getattr(S, f"shmem_{args.dtype}_{args.op}_reduce")
     team = S.team_world()
-
-    def step():
-        fn(team, dst.data_ptr(), src.data_ptr(), n)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    dist.barrier()
-    el = torch.tensor([t1 - t0], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    t_step = el.item() / args.steps
-
-    # phase split (separate calls, so the timed loop above carries no events)
-    S.prof_enable(True)
-    for _ in range(3):
-        step()
-    prof = S.prof_get()
-    S.prof_enable(False)
-
-    mismatches = self_check(torch, L, S, dt, L.op_id(args.op), dist_kind, seed, world, n, es, alg,
-                            dst, stream)
-    mm = torch.tensor([mismatches], dtype=torch.int64)
-    dist.all_reduce(mm, op=dist.ReduceOp.SUM)
-
     resolved = S.lib().sosx_resolve_alg(alg, n * es, 16384)
     name = {v: k for k, v in L.ALGS.items()}[resolved]
-    fold_ms = prof["fold_ms"] / max(prof["nfold"], 1)
-    xfer_ms = prof["xfer_ms"] / max(prof["ncall"], 1)
     P = world
+
+    def step():
+        fn(team, dst, src, n)
+
+    results = {}
+    for tname, tid in (("rccl", 0), ("p2p", 1)):
+        if S.lib().shmemx_set_transport(tid) < 0:
+            results[tname] = {"available": False}
+            continue
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        dist.barrier()
+        el = torch.tensor([t1 - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        t_step = el.item() / args.steps
+        # phase split (separate calls, so the timed loop carries no events)
+        S.prof_enable(True)
+        for _ in range(3):
+            step()
+        prof = S.prof_get()
+        S.prof_enable(False)
+        mm = self_check(torch, L, S, dt, L.op_id(args.op), dist_kind, seed, world, n, es, alg, dst,
+                        stream)
+        mmt = torch.tensor([mm], dtype=torch.int64)
+        dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
+        results[tname] = {"t_step": t_step, "prof": prof, "mismatches": int(mmt.item())}
+
+    primary = "rccl" if results["rccl"].get("available", True) else "p2p"
+    r = results[primary]
+    t_step, prof = r["t_step"], r["prof"]
+    fold_ms = prof["fold_ms"] / max(prof["nfold"], 1)
     if resolved in (L.ALGS["ring"], L.ALGS["recdbl_direct"]):
         fold_bytes = (P + 1) * (n // P) * es       # P inputs of one chunk + the output
     else:
         fold_bytes = 3 * (n // 2) * es             # first (largest) pairwise step
     wire = 2 * (P - 1) / P * n * es if resolved != L.ALGS["recdbl"] else (P.bit_length() - 1) * n * es
+
+    def team_roof(rr):
+        ts = rr["t_step"]
+        return {"ms_per_step": round(ts * 1e3, 4),
+                "value_GiBs": round(world * n * es / ts / GiB, 3),
+                "busbw_GBs": round(wire / ts / 1e9, 1),
+                "frac_one_link": round(wire / ts / 1e9 / XGMI_LINK_GBS, 3),
+                "frac_7_links": round(wire / ts / 1e9 / (XGMI_LINK_GBS * XGMI_LINKS), 3),
+                "xfer_ms_per_step": round(rr["prof"]["xfer_ms"] / max(rr["prof"]["ncall"], 1), 4),
+                "fold_ms_per_step": round(rr["prof"]["fold_ms"] / max(rr["prof"]["ncall"], 1), 4),
+                "bitwise_mismatches_all_ranks": rr["mismatches"]}
+
     res = {
         "metric": "GiB/s device-resident sum_reduce combine, nreduce=128Mi fp32; 1/2/4/8 GPU",
         "value": round(world * n * es / t_step / GiB, 3),
@@ -109,26 +134,28 @@ def main(args, torch):
         "dtype": {"float": "f32", "double": "f64"}.get(args.dtype, args.dtype),
         "data": "synthetic (splitmix64 counter hash per PE, SURVEY.md 8(d)), resident in HBM",
         "config": {"workload": f"shmem_{args.dtype}_{args.op}_reduce(SHMEM_TEAM_WORLD) nreduce={n} "
-                               f"per PE, {world} PEs (1 per MI355X), RCCL over xGMI + HIP fold",
-                   "nreduce": n, "algorithm": name, "parallelism": f"pe{world}"},
+                               f"per PE, {world} PEs (1 per MI355X), "
+                               + ("RCCL over xGMI + HIP fold" if primary == "rccl" else
+                                  "p2p reads of IPC-mapped peer HBM + HIP fold"),
+                   "nreduce": n, "algorithm": name, "transport": primary,
+                   "parallelism": f"pe{world}"},
         "roofline": {"bound": "hbm", "kernel": "sos::k_fold (fused P-way combine)",
                      "achieved": round(fold_bytes / (fold_ms / 1e3) / 1e9, 1) if fold_ms > 0 else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(fold_bytes / (fold_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if fold_ms > 0 else None,
                      "traffic": None, "algorithmic_bytes_per_launch": fold_bytes,
                      "mean_kernel_ms": round(fold_ms, 5)},
-        "team_roofline": {"bound": "xgmi", "wire_bytes_per_pe": int(wire),
-                          "busbw_GBs": round(wire / t_step / 1e9, 1),
-                          "frac_one_link": round(wire / t_step / 1e9 / XGMI_LINK_GBS, 3),
-                          "frac_7_links": round(wire / t_step / 1e9 / (XGMI_LINK_GBS * XGMI_LINKS), 3),
-                          "xfer_ms_per_step": round(xfer_ms, 4), "fold_ms_per_step":
-                          round(prof["fold_ms"] / max(prof["ncall"], 1), 4)},
-        "check": {"bitwise_mismatches_all_ranks": int(mm.item()),
+        "team_roofline": dict(bound="xgmi", wire_bytes_per_pe=int(wire), **team_roof(r)),
+        "check": {"bitwise_mismatches_all_ranks": r["mismatches"],
                   "against": "on-GPU regeneration of all PE inputs + schedule-order fold"},
     }
+    if primary == "rccl" and results["p2p"].get("available", True):
+        res["p2p_transport"] = team_roof(results["p2p"])
     if rank == 0:
         print(json.dumps(res), flush=True)
     dist.barrier()
+    S.shmemx_free_device(dst)
+    S.shmemx_free_device(src)
     S.shmem_finalize()
     dist.destroy_process_group()
     return 0
@@ -155,6 +182,6 @@ def self_check(torch, L, S, dt, opid, dist_kind, seed, world, n, es, alg, dst, s
     else:
         L.fold(opid, dt, L.ORDER_TREE, exp.data_ptr(), [b.data_ptr() for b in ins], n, stream)
     torch.cuda.synchronize()
-    bad = L.count_mismatch(exp.data_ptr(), dst.data_ptr(), n, es, stream)
+    bad = L.count_mismatch(exp.data_ptr(), dst, n, es, stream)
     del ins
     return bad

@@ -7,6 +7,7 @@ memory -- the same code that reads xGMI peer memory on the 8-GPU node.  (RCCL re
 two ranks on one GPU, so the RCCL transport's multi-PE runs are the 8-GPU bench's.)
 """
 import os
+import re
 import subprocess
 import sys
 
@@ -57,5 +58,6 @@ def test_reduce_types_4_pes(examples):
 @pytest.mark.parametrize("np_", [2, 3, 4, 8])
 def test_team_check(np_):
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900)
-    ok = [ln for ln in r.stdout.splitlines() if "checks OK" in ln]
-    assert r.returncode == 0 and len(ok) == np_, r.stdout + r.stderr[-3000:]
+    # PEs print concurrently, so lines may interleave: count the reports, not lines
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
+    assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
