@@ -245,17 +245,41 @@ void ensure_device_heap()
     s.p2p_ready = s.n_pes == 1;
     if (!s.want_p2p || s.n_pes == 1) return;
     if (!s.hub.up) raise_error("SHMEMX_TRANSPORT=p2p needs the shmem_init bootstrap");
+    // p2p-only mode cannot run without the mapping; in `both` mode a failure on any PE
+    // turns the p2p transport off on every PE (agreed through the hub)
+    const bool fatal = s.transport == TRANSPORT_P2P;
     hipIpcMemHandle_t mine;
-    hip_check(hipIpcGetMemHandle(&mine, base), "hipIpcGetMemHandle(device heap)");
+    memset(&mine, 0, sizeof(mine));
+    hipError_t e = hipIpcGetMemHandle(&mine, base);
+    if (e != hipSuccess && fatal) hip_check(e, "hipIpcGetMemHandle(device heap)");
     std::vector<hipIpcMemHandle_t> all((size_t)s.n_pes);
     if (sosboot::hub_allgather(&s.hub, &mine, sizeof(mine), all.data()) != 0)
         raise_error("device heap: IPC handle exchange failed");
-    for (int q = 0; q < s.n_pes; ++q) {
+    int ok = e == hipSuccess;
+    for (int q = 0; q < s.n_pes && ok; ++q) {
         if (q == s.my_pe) continue;
         void *p = nullptr;
-        hip_check(hipIpcOpenMemHandle(&p, all[(size_t)q], hipIpcMemLazyEnablePeerAccess),
-                  "hipIpcOpenMemHandle(peer device heap)");
+        hipError_t eo = hipIpcOpenMemHandle(&p, all[(size_t)q], hipIpcMemLazyEnablePeerAccess);
+        if (eo != hipSuccess) {
+            if (fatal) hip_check(eo, "hipIpcOpenMemHandle(peer device heap)");
+            (void)hipGetLastError();
+            warn("cannot map PE %d's device heap (%s): p2p transport off", q, hipGetErrorString(eo));
+            ok = 0;
+            break;
+        }
         s.peer_heap[(size_t)q] = (char *)p;
+    }
+    std::vector<int> oks((size_t)s.n_pes);
+    if (sosboot::hub_allgather(&s.hub, &ok, sizeof(ok), oks.data()) != 0)
+        raise_error("device heap: mapping agreement failed");
+    for (int v : oks) ok &= v;
+    if (!ok) {
+        for (int q = 0; q < s.n_pes; ++q)
+            if (q != s.my_pe && s.peer_heap[(size_t)q]) {
+                (void)hipIpcCloseMemHandle(s.peer_heap[(size_t)q]);
+                s.peer_heap[(size_t)q] = nullptr;
+            }
+        return;
     }
     s.p2p_ready = true;
     debug_msg("device heap %zu B (stage %zu B) mapped on %d PEs", s.dev_heap_bytes,

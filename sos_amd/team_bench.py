@@ -93,8 +93,17 @@ def main(args, torch):
             step()
         prof = S.prof_get()
         S.prof_enable(False)
-        mm = self_check(torch, L, S, dt, L.op_id(args.op), dist_kind, seed, world, n, es, alg, dst,
-                        stream)
+        # fresh inputs for the checked call: a transport that returned bytes left over
+        # from the timed loop (same inputs every step) would fail here
+        check_seed = seed + 1 + tid
+        L.fill(dt, dist_kind, check_seed, rank, src, n, 0, stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        step()
+        mm = self_check(torch, L, S, dt, L.op_id(args.op), dist_kind, check_seed, world, n, es,
+                        alg, dst, stream)
+        L.fill(dt, dist_kind, seed, rank, src, n, 0, stream)
+        torch.cuda.synchronize()
         mmt = torch.tensor([mm], dtype=torch.int64)
         dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
         results[tname] = {"t_step": t_step, "prof": prof, "mismatches": int(mmt.item())}
