@@ -191,7 +191,6 @@ void op_to_all(void *target, const void *source, size_t count, size_t ts, const 
         return;
     }
     int rc = sos_check_op(op, dt);
-    if (rc == SOSX_OK && sos_dtype_info(dt).kind == K_LDBL) rc = SOSX_ERR_UNSUPPORTED;
     if (rc) raise_error("%s: %s (datatype %d, op %d)", fn, status_text(rc), dt, op);
 
     int alg = sosplan::resolve_alg(s.reduce_alg, bytes, s.coll_size_crossover);
@@ -355,7 +354,6 @@ int sosx_loopback_allreduce(int alg, int P, int op, int datatype, void *const *s
     if (P < 1 || P > SOSX_MAX_FOLD || !srcs || !dsts) return SOSX_ERR_ARG;
     int rc = sos_check_op(op, datatype);
     if (rc) return rc;
-    if (sos_dtype_info(datatype).kind == K_LDBL && P > 1) return SOSX_ERR_UNSUPPORTED;
     const size_t ts = sos_dtype_info(datatype).size;
     hipStream_t sm = (hipStream_t)stream;
     const int a = sosplan::resolve_alg(alg, count * ts, 16384);

@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "dtypes.h"
+#include "ldbl.h"
 #include "sosx.h"
 
 #pragma clang fp contract(off)
@@ -111,11 +112,22 @@ struct OpXor {
     template <class T> __device__ __forceinline__ static T f(T a, T b) { return (T)(a ^ b); }
 };
 // (a) > (b) ? (a) : (b) -- returns `in` on ties and whenever a compare is unordered.
+// long double: the chosen operand's 10 value bytes, the left operand's padding.
 struct OpMax {
     template <class T> __device__ __forceinline__ static T f(T a, T b) { return a > b ? a : b; }
+    __device__ __forceinline__ static ld80 f(ld80 a, ld80 b)
+    {
+        const ld80 &c = x87::gt(a, b) ? a : b;
+        return x87::make(a, x87::se(c), c.m);
+    }
 };
 struct OpMin {
     template <class T> __device__ __forceinline__ static T f(T a, T b) { return a < b ? a : b; }
+    __device__ __forceinline__ static ld80 f(ld80 a, ld80 b)
+    {
+        const ld80 &c = x87::gt(b, a) ? a : b;  // (a) < (b) ? (a) : (b)
+        return x87::make(a, x87::se(c), c.m);
+    }
 };
 struct OpSum {
     template <class T> __device__ __forceinline__ static T f(T a, T b)
@@ -140,6 +152,7 @@ struct OpSum {
     {
         return cf64{x86_add(a.re, b.re), x86_add(b.im, a.im)};
     }
+    __device__ __forceinline__ static ld80 f(ld80 a, ld80 b) { return x87::add(a, b); }
 };
 struct OpProd {
     template <class T> __device__ __forceinline__ static T f(T a, T b)
@@ -164,6 +177,7 @@ struct OpProd {
         cmul<double>(a.re, a.im, b.re, b.im, r.re, r.im);
         return r;
     }
+    __device__ __forceinline__ static ld80 f(ld80 a, ld80 b) { return x87::mul(a, b); }
 };
 
 // ---------------------------------------------------------------------------------
@@ -284,7 +298,7 @@ inline int dispatch(int op, int dt, A... args)
         case K_C64:
             return op == SOSX_OP_SUM ? F::template run<cf64, OpSum>(args...)
                                      : F::template run<cf64, OpProd>(args...);
-        case K_LDBL: return SOSX_ERR_UNSUPPORTED;
+        case K_LDBL: SOS_FP_CASES(ld80)
         default: return SOSX_ERR_DTYPE;
     }
 #undef SOS_INT_CASES

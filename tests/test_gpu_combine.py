@@ -202,3 +202,72 @@ def test_fill_matches_oracle(torch_cuda, sos, oracle):
             sos.fill(dt, dist, 1234, 3, buf.data_ptr(), n, 77)
             torch.cuda.synchronize()
             assert same_bits(from_dev(buf, 0, ref), ref), (dt, dist)
+
+
+# ---------------------------------------------------------------------------------
+# long double: software x87 80-bit arithmetic on the GPU vs the CPU's x87 (oracle)
+# ---------------------------------------------------------------------------------
+def longdouble_inputs(n, rng):
+    ld = np.longdouble
+    mant = rng.standard_normal(n).astype(ld) + rng.standard_normal(n).astype(ld) * ld(2.0) ** -40
+    a = np.ldexp(mant, rng.integers(-16300, 16300, n))
+    small = np.ldexp(mant, rng.integers(-16460, -16370, n))       # denormal range
+    pool = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0], dtype=ld)
+    pool = np.concatenate([pool, [np.finfo(ld).max, -np.finfo(ld).max, np.finfo(ld).tiny,
+                                  np.finfo(ld).tiny / ld(8)]])
+    pick = rng.random(n)
+    a = np.where(pick < 0.2, small, a)
+    sp = rng.random(n) < 0.1
+    a[sp] = rng.choice(pool, sp.sum())
+    return a.astype(ld)
+
+
+def ld_equal(got, ref):
+    g = got.view(np.uint8).reshape(-1, 16)
+    r = ref.view(np.uint8).reshape(-1, 16)
+    same = np.all(g == r, axis=1)
+    both_nan = np.isnan(got) & np.isnan(ref)
+    return same | both_nan
+
+
+@pytest.mark.parametrize("op", [3, 4, 5, 6])
+def test_longdouble_combine_vs_x87(torch_cuda, sos, oracle, op):
+    torch = torch_cuda
+    rng = np.random.default_rng(80 + op)
+    n = 20000
+    a = longdouble_inputs(n, rng)
+    b = longdouble_inputs(n, rng)
+    # cancellation and near-overflow pairs
+    b[:500] = -a[:500]
+    b[500:1000] = -a[500:1000] * (1 + np.ldexp(np.longdouble(1), -63))
+    b[1000:1500] = a[1000:1500]
+    ref = a.copy()
+    oracle.reduce_local(op, 25, b, ref)
+    da, pa = to_dev(torch, a)
+    db, pb = to_dev(torch, b)
+    sos.combine(op, 25, pa, pb, n)
+    torch.cuda.synchronize()
+    got = from_dev(da, 0, a)
+    ok = ld_equal(got, ref)
+    bad = np.nonzero(~ok)[0]
+    assert bad.size == 0, [(repr(a[i]), repr(b[i]), repr(got[i]), repr(ref[i])) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("alg", ["ring", "recdbl"])
+def test_longdouble_team_loopback(torch_cuda, sos, oracle, alg):
+    from sos_amd import shmem as S
+    torch = torch_cuda
+    rng = np.random.default_rng(7)
+    for P in (2, 3, 5):
+        n = 3001
+        srcs = [np.ldexp(rng.standard_normal(n).astype(np.longdouble), rng.integers(-30, 30, n))
+                for _ in range(P)]
+        for op in (5, 6, 4):
+            ref = (oracle.ring if alg == "ring" else oracle.recdbl)(op, 25, srcs)
+            sb = [to_dev(torch, s)[0] for s in srcs]
+            db = [torch.zeros_like(x) for x in sb]
+            S.loopback_allreduce(alg, op, 25, [x.data_ptr() for x in sb], [x.data_ptr() for x in db], n)
+            torch.cuda.synchronize()
+            for p in range(P):
+                got = from_dev(db[p], 0, srcs[p])
+                assert ld_equal(got, ref[p]).all(), (alg, P, op, p)
