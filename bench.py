@@ -162,12 +162,14 @@ def host_resident(args, torch):
     out = {}
     da = torch.empty(n * es, dtype=torch.uint8, device="cuda")
     db = torch.empty_like(da)
+    lib = L.lib()
     for kind in ("pinned", "pageable"):
         ha = torch.empty(n * es, dtype=torch.uint8, pin_memory=(kind == "pinned"))
         hb = torch.empty(n * es, dtype=torch.uint8, pin_memory=(kind == "pinned"))
         ha.fill_(0)
         hb.fill_(0)
         reps = 5
+        # serial: copy both in, combine, copy out
         for r in range(reps + 1):
             if r == 1:
                 torch.cuda.synchronize()
@@ -178,12 +180,21 @@ def host_resident(args, torch):
             ha.copy_(da, non_blocking=True)
             torch.cuda.synchronize()
         t = (time.perf_counter() - t0) / reps
-        out[f"{kind}_GiBs"] = round(n * es / t / GiB, 3)
-        out[f"{kind}_ms"] = round(t * 1e3, 3)
+        out[f"{kind}_serial_GiBs"] = round(n * es / t / GiB, 3)
+        # pipelined: sosx_combine_host (what shmemx_reduce_local does for host operands)
+        for r in range(reps + 1):
+            if r == 1:
+                t0 = time.perf_counter()
+            L.check(lib.sosx_combine_host(L.op_id(args.op), dt, ha.data_ptr(), hb.data_ptr(), n, 0),
+                    "sosx_combine_host")
+        t = (time.perf_counter() - t0) / reps
+        out[f"{kind}_pipelined_GiBs"] = round(n * es / t / GiB, 3)
+        out[f"{kind}_pipelined_ms"] = round(t * 1e3, 3)
         del ha, hb
     out["bytes_moved_per_call"] = {"H2D": 2 * n * es, "D2H": n * es}
     out["note"] = ("payload GiB/s of reduce_local on host-resident operands through the GPU: "
-                   "H2D(inout, in) + combine + D2H(inout); PCIe Gen5 x16 = 63 GB/s spec")
+                   "H2D(inout, in) + combine + D2H(inout); serial vs 3-stream chunk pipeline "
+                   "(sosx_combine_host); PCIe Gen5 x16 = 63 GB/s per direction (spec)")
     return out
 
 

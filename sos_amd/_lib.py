@@ -63,6 +63,8 @@ _SIGS = {
     "sosx_count_mismatch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_size_t,
                                        _c.POINTER(_c.c_ulonglong), _c.c_void_p]),
     "sosx_memcpy": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    "sosx_combine_host": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_size_t,
+                                     _c.c_size_t]),
     "sosx_set_combine_variant": (_c.c_int, [_c.c_int]),
     "sosx_num_combine_variants": (_c.c_int, []),
     "sosx_combine_variant_name": (_c.c_char_p, [_c.c_int]),

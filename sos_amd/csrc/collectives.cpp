@@ -327,6 +327,9 @@ int sos_api_reduce(shmem_team_t team, void *dest, const void *source, size_t nre
 int shmemx_reduce_local(int op, int datatype, size_t count, const void *in, void *inout)
 {
     check_initialized("shmemx_reduce_local");
+    // host operands (the SOS heap): pipelined over PCIe; device operands: one kernel
+    if (!is_device_ptr(inout) && !is_device_ptr(in))
+        return sosx_combine_host(op, datatype, inout, in, count, 0);
     return sosx_combine(op, datatype, inout, in, count, st().stream);
 }
 

@@ -271,3 +271,23 @@ def test_longdouble_team_loopback(torch_cuda, sos, oracle, alg):
             for p in range(P):
                 got = from_dev(db[p], 0, srcs[p])
                 assert ld_equal(got, ref[p]).all(), (alg, P, op, p)
+
+
+@pytest.mark.parametrize("dt,op", [(23, 5), (24, 6), (11, 2), (27, 6), (25, 5)])
+def test_combine_host_pipeline(torch_cuda, sos, oracle, dt, op):
+    """Host-resident operands through the chunked H2D || combine || D2H pipeline."""
+    import ctypes
+    rng = np.random.default_rng(dt + op)
+    for n, chunk in ((1, 0), (100003, 4096), (3 * 1024 * 1024 + 7, 1 << 20)):
+        if dt == 25:
+            a = np.ldexp(rng.standard_normal(n).astype(np.longdouble), rng.integers(-9, 9, n))
+            b = np.ldexp(rng.standard_normal(n).astype(np.longdouble), rng.integers(-9, 9, n))
+        else:
+            a, b = make_inputs(oracle, dt, op, n, rng, False)
+        ref = a.copy()
+        oracle.reduce_local(op, dt, b, ref)
+        got = a.copy()
+        rc = sos.lib().sosx_combine_host(op, dt, got.ctypes.data_as(ctypes.c_void_p),
+                                         b.ctypes.data_as(ctypes.c_void_p), n, chunk)
+        assert rc == 0
+        assert check(dt, op, got, ref), (dt, op, n, chunk)
