@@ -3,10 +3,10 @@
 //
 // A 3-stream elementwise pass (read in, read inout, write inout; 1 op per element) is
 // HBM-bandwidth bound.  The kernel is built for the HBM roofline:
-//   * 16-byte (dwordx4) loads/stores per lane, U=4 vectors per lane per operand, all
-//     2U loads of a tile issued before the first combine (8 x 16 B in flight/lane);
-//   * 256-thread workgroups, one 16 KiB-per-operand tile per workgroup, >> 256
-//     workgroups per launch (a 128Mi fp32 combine is 32768 workgroups), the ragged
+//   * 16-byte (dwordx4) nontemporal loads/stores per lane, U vectors per lane per
+//     operand (default U=1), all 2U loads of a tile issued before the first combine;
+//   * 256-thread workgroups, one 4 KiB-per-operand tile per workgroup, >> 256
+//     workgroups per launch (a 128Mi fp32 combine is 131072 workgroups), the ragged
 //     head/tail handled by one extra workgroup so the hot tiles carry no bounds checks;
 //   * relative 16-B misalignment of the operands falls back to element loads.
 // Tuning variants (bench.py --variants) are compiled for the fp32 sum only.
@@ -35,6 +35,43 @@ __global__ __launch_bounds__(kThreads) void k_combine3(T *__restrict__ out, cons
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) stv<NTS>(O + base + u * kThreads, apply<T, OP>(ra[u], rb[u]));
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n;
+             i += kThreads)
+            out[i] = OP::f(a[i], b[i]);
+    }
+}
+
+// Buffer-descriptor variant: raw_buffer_load/store_b128 with explicit cache-policy
+// bits (gfx950 aux: sc0 = 1, nt = 2, sc1 = 16), one wave-uniform descriptor per tile.
+// Tuning variants only (bench --variants).
+template <class T, class OP, int U, int AUXL, int AUXS>
+__global__ __launch_bounds__(kThreads) void k_combine3_buf(T *__restrict__ out, const T *a,
+                                                             const T *b, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    constexpr int kTileBytes = kThreads * U * 16;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t tb = t * (size_t)kTileBytes;
+        auto rA = __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)(a + g.head) + tb), 0,
+                                                    kTileBytes, 0x00020000);
+        auto rB = __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)(b + g.head) + tb), 0,
+                                                    kTileBytes, 0x00020000);
+        auto rO = __builtin_amdgcn_make_buffer_rsrc((void *)((char *)(out + g.head) + tb), 0,
+                                                    kTileBytes, 0x00020000);
+        u32x4 ra[U], rb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int off = (int)(threadIdx.x + u * kThreads) * 16;
+            ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rA, off, 0, AUXL);
+            rb[u] = __builtin_amdgcn_raw_buffer_load_b128(rB, off, 0, AUXL);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(apply<T, OP>(ra[u], rb[u]), rO,
+                                                   (int)(threadIdx.x + u * kThreads) * 16, 0, AUXS);
     }
     if (g.has_rem && blockIdx.x == gridDim.x - 1) {
         for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
@@ -107,8 +144,8 @@ struct VariantDesc {
     const char *name;
 };
 const VariantDesc kVariants[] = {
-    {"u4_nt"},             // 0: default: U=4, nontemporal loads+stores, one tile/workgroup
-    {"u1_nt"},             // 1
+    {"u1_nt"},             // 0: default: U=1, nontemporal loads+stores, one tile/workgroup
+    {"u4_nt"},             // 1: U=4 (round-1 default until the A/B in profiles/r1_combine_variants*)
     {"u2_nt"},             // 2
     {"u8_nt"},             // 3
     {"u4_ntload"},         // 4: nontemporal loads, plain stores
@@ -117,6 +154,11 @@ const VariantDesc kVariants[] = {
     {"u4_nt_persist4096"}, // 7: grid-stride over 4096 workgroups
     {"u2_nt_persist2048"}, // 8
     {"u4_lds_dma"},        // 9: partner tile via global_load_lds (LDS-DMA)
+    {"buf_u4_nt"},         // 10: buffer loads/stores, aux nt
+    {"buf_u4_plainld_ntst"},  // 11
+    {"buf_u4_sc1nt"},      // 12: aux sc1|nt both ways
+    {"buf_u2_nt"},         // 13
+    {"buf_u1_nt"},         // 14
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -145,7 +187,7 @@ int launch_combine3(T *out, const T *a, const T *b, size_t n, hipStream_t st)
     }
     if constexpr (std::is_same<T, float>::value && std::is_same<OP, OpSum>::value) {
         switch (g_variant) {
-            case 1: return launch_combine3_vec<T, OP, 1, true, true>(out, a, b, n, st, kNoCap);
+            case 1: return launch_combine3_vec<T, OP, 4, true, true>(out, a, b, n, st, kNoCap);
             case 2: return launch_combine3_vec<T, OP, 2, true, true>(out, a, b, n, st, kNoCap);
             case 3: return launch_combine3_vec<T, OP, 8, true, true>(out, a, b, n, st, kNoCap);
             case 4: return launch_combine3_vec<T, OP, 4, true, false>(out, a, b, n, st, kNoCap);
@@ -159,12 +201,24 @@ int launch_combine3(T *out, const T *a, const T *b, size_t n, hipStream_t st)
                                    dim3(kThreads), 0, st, out, a, b, g);
                 return hip_ok(hipGetLastError());
             }
+            case 10: case 11: case 12: case 13: case 14: {
+                const int U = g_variant == 13 ? 2 : g_variant == 14 ? 1 : 4;
+                Geom g = make_geom(o, n, sizeof(T), U);
+                dim3 gr(grid_for(g, kNoCap)), bl(kThreads);
+                if (g_variant == 10) hipLaunchKernelGGL((k_combine3_buf<T, OP, 4, 2, 2>), gr, bl, 0, st, out, a, b, g);
+                if (g_variant == 11) hipLaunchKernelGGL((k_combine3_buf<T, OP, 4, 0, 2>), gr, bl, 0, st, out, a, b, g);
+                if (g_variant == 12) hipLaunchKernelGGL((k_combine3_buf<T, OP, 4, 18, 18>), gr, bl, 0, st, out, a, b, g);
+                if (g_variant == 13) hipLaunchKernelGGL((k_combine3_buf<T, OP, 2, 2, 2>), gr, bl, 0, st, out, a, b, g);
+                if (g_variant == 14) hipLaunchKernelGGL((k_combine3_buf<T, OP, 1, 2, 2>), gr, bl, 0, st, out, a, b, g);
+                return hip_ok(hipGetLastError());
+            }
             default: break;
         }
     }
-    // Default: U=4, nontemporal loads and stores (measured 80.5% vs 70.5% of the 8 TB/s
-    // HBM peak for plain loads/stores on the 128Mi fp32 sum; profiles/r1_*).
-    return launch_combine3_vec<T, OP, 4, true, true>(out, a, b, n, st, kNoCap);
+    // Default: U=1 (one 16-B vector per lane per operand, 4 KiB tiles), nontemporal loads
+    // and stores: nt is worth +16% over plain loads/stores, U=1 ~2% over U=4 in two
+    // independent A/B runs on the 128Mi fp32 sum (profiles/r1_combine_variants*.txt).
+    return launch_combine3_vec<T, OP, 1, true, true>(out, a, b, n, st, kNoCap);
 }
 
 struct Combine3Fn {
