@@ -116,11 +116,28 @@ SHMEM_FUNCTION_ATTRIBUTES void shmem_sync(int PE_start, int logPE_stride, int PE
 SHMEM_FUNCTION_ATTRIBUTES void shmem_barrier(int PE_start, int logPE_stride, int PE_size,
                                              long *pSync);
 
+/* broadcast (src/collectives_c.c4:342-400): the active-set forms leave the root's
+ * target untouched; the team form also copies source to dest on the root */
+SHMEM_FUNCTION_ATTRIBUTES void shmem_broadcast32(void *target, const void *source, size_t nlong,
+                                                 int PE_root, int PE_start, int logPE_stride,
+                                                 int PE_size, long *pSync);
+SHMEM_FUNCTION_ATTRIBUTES void shmem_broadcast64(void *target, const void *source, size_t nlong,
+                                                 int PE_root, int PE_start, int logPE_stride,
+                                                 int PE_size, long *pSync);
+SHMEM_FUNCTION_ATTRIBUTES int shmem_broadcastmem(shmem_team_t team, void *dest, const void *source,
+                                                 size_t nelems, int PE_root);
+void pshmem_broadcast32(void *target, const void *source, size_t nlong, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync);
+void pshmem_broadcast64(void *target, const void *source, size_t nlong, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync);
+int pshmem_broadcastmem(shmem_team_t team, void *dest, const void *source, size_t nelems,
+                        int PE_root);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif
 
-/* ---- the reduction family (generated: sos_amd/csrc/gen_bindings.py) ------- */
+/* ---- the reduction family + typed broadcasts (generated: gen_bindings.py) --- */
 #include "shmem_reductions.h"
 
 #endif /* SHMEM_H */

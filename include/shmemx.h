@@ -31,6 +31,9 @@
 extern "C" {
 #endif
 
+/* the PEs of this node (src/shmem_team.c:101-164); one node per job in this build */
+extern shmem_team_t SHMEMX_TEAM_NODE;
+
 SHMEM_FUNCTION_ATTRIBUTES void shmemx_heap_create(void *base, size_t size, int device_type,
                                                   int device_index);
 SHMEM_FUNCTION_ATTRIBUTES void *shmemx_malloc_device(size_t size);
@@ -62,7 +65,10 @@ SHMEM_FUNCTION_ATTRIBUTES int shmemx_set_reduce_algorithm(int alg);
 
 /* Single-GPU loopback team (tests/validation): run the SOS team reduction of P
  * simulated PEs whose source/target buffers all live on this device, with the same
- * per-PE plans the RCCL executor runs and device-to-device copies as the transport. */
+ * per-PE plans the RCCL executor runs and device-to-device copies as the transport.
+ * `alg` may also be SOSX_PLAN_INSCAN / SOSX_PLAN_EXSCAN (the team scans) or
+ * SOSX_PLAN_BCAST(root, copy_root) (broadcast; op ignored, datatype sets the element
+ * size). */
 SHMEM_FUNCTION_ATTRIBUTES int sosx_loopback_allreduce(int alg, int P, int op, int datatype,
                                                       void *const *srcs, void *const *dsts,
                                                       size_t count, void *stream);
@@ -70,5 +76,8 @@ SHMEM_FUNCTION_ATTRIBUTES int sosx_loopback_allreduce(int alg, int P, int op, in
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif
+
+/* ---- team prefix sums (generated: sos_amd/csrc/gen_bindings.py) ------------- */
+#include "shmemx_scans.h"
 
 #endif /* SHMEMX_H */

@@ -115,8 +115,23 @@ int sosx_combine3(int op, int dtype, void *out, const void *a, const void *b, si
  * nin <= SOSX_MAX_FOLD.  This is the fused P-way combine used by the team schedules.
  */
 #define SOSX_MAX_FOLD 64
+
+/* Plan ids of the non-reduction team collectives (scans, broadcast) that share the
+ * reduction's plan executors (sosx_loopback_allreduce, sosx_plan_encode). */
+#define SOSX_PLAN_INSCAN 16
+#define SOSX_PLAN_EXSCAN 17
+#define SOSX_PLAN_BCAST(root, copy_root) (32 + 2 * (root) + ((copy_root) ? 1 : 0))
 int sosx_fold(int op, int dtype, int order, void *out, const void *const *ins, int nin,
               size_t count, void *stream);
+
+/*
+ * Fused prefix: outs[k][i] = ins[0][i] OP ins[1][i] OP ... OP ins[k][i] (the running
+ * prefix is the left operand), k < np <= 64 -- the local step of the team scans.
+ * `own` (or -1) is the one input allowed to alias an output for np > 8; for np <= 8 any
+ * input may alias any output.
+ */
+int sosx_prefix(int op, int dtype, void *const *outs, const void *const *ins, int np, int own,
+                size_t count, void *stream);
 
 /* Fill `count` elements of device buffer dst with the synthetic input of PE `pe`,
  * element indices [index0, index0 + count).  Bit-identical to the CPU generator

@@ -40,6 +40,10 @@ def lib():
         L.oracle_ring.restype = i
         L.oracle_recdbl.argtypes = [i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
         L.oracle_recdbl.restype = i
+        L.oracle_scan.argtypes = [i, sz, i, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.oracle_scan.restype = i
+        L.oracle_bcast.argtypes = [i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.oracle_bcast.restype = i
         L.oracle_fill.argtypes = [i, i, ctypes.c_uint64, i, vp, sz, sz]
         L.oracle_fill.restype = i
         L.oracle_time_reduce_local.argtypes = [i, i, i, vp, vp, i]
@@ -95,6 +99,30 @@ def recdbl(op, dt, srcs, dsts=None):
     if dsts is None:
         dsts = [np.zeros_like(a) for a in srcs]
     return _team(lib().oracle_recdbl, op, dt, srcs, dsts)
+
+
+def scan(op, dt, srcs, exclusive, dsts=None):
+    """SOS team prefix scan (src/collectives.c:1111-1209) over P simulated PEs."""
+    if dsts is None:
+        dsts = [np.zeros_like(a) for a in srcs]
+    P = len(srcs)
+    s = (ctypes.c_void_p * P)(*[a.ctypes.data for a in srcs])
+    d = (ctypes.c_void_p * P)(*[a.ctypes.data for a in dsts])
+    rc = lib().oracle_scan(P, srcs[0].size, op, dt, 1 if exclusive else 0, s, d)
+    if rc:
+        raise ValueError(f"oracle_scan rc={rc}")
+    return dsts
+
+
+def bcast(srcs, root, copy_root, dsts):
+    """SOS broadcast (src/collectives.c:429-485) over P simulated PEs, in place on dsts."""
+    P = len(srcs)
+    s = (ctypes.c_void_p * P)(*[a.ctypes.data for a in srcs])
+    d = (ctypes.c_void_p * P)(*[a.ctypes.data for a in dsts])
+    rc = lib().oracle_bcast(P, srcs[0].nbytes, root, 1 if copy_root else 0, s, d)
+    if rc:
+        raise ValueError(f"oracle_bcast rc={rc}")
+    return dsts
 
 
 def time_reduce_local(op, dt, inp, inout, reps):

@@ -19,6 +19,8 @@
  *                           op macros :37-43, dtype classes :225-303)
  *   oracle_ring          -- src/collectives.c:647-764 (P PEs simulated in one process)
  *   oracle_recdbl        -- src/collectives.c:850-984 (P PEs simulated in one process)
+ *   oracle_scan          -- src/collectives.c:1111-1209 (inscan / exscan, P PEs)
+ *   oracle_bcast         -- src/collectives.c:429-485 + src/collectives_c.c4:342-429
  *   oracle_*_time        -- single-core timing helpers for bench.py's cpu_baseline
  */
 #include <stddef.h>
@@ -238,6 +240,54 @@ int oracle_recdbl(int P, size_t count, int op, int dt, void **src, void **dst)
     for (int p = 0; p < P; p++) free(cur[p]);
     free(cur);
     return rc;
+}
+
+/* ------------------------------------------------------------------------------
+ * Team prefix scans, src/collectives.c:1111-1209 (scan_ring).  In-place calls work on
+ * a copy of the source (:1123-1134).  PE_start zeroes its own target for exscan
+ * (:1145-1155) and puts its source into the targets of team PEs exclusive..P-1
+ * (:1158-1166); then PE 1, 2, ... in turn (each waits for its left neighbour's
+ * pSync, :1181-1185) apply target = target OP source -- shmem_internal_atomicv, the
+ * running target is the left operand -- to the targets of PEs i+exclusive..P-1
+ * (:1188-1196).  scan_linear (:991-1108) posts the same atomics without the ordering;
+ * its result is this one whenever OP is associative and commutative on the values.
+ * ------------------------------------------------------------------------------ */
+int oracle_scan(int P, size_t count, int op, int dt, int exclusive, void **src, void **dst)
+{
+    size_t ts = oracle_type_size(dt), bytes;
+    if (!ts) return -1;
+    if (count == 0) return 0;
+    bytes = count * ts;
+    void **in = malloc(sizeof(void *) * P);
+    for (int p = 0; p < P; p++) { in[p] = malloc(bytes); memcpy(in[p], src[p], bytes); }
+    if (exclusive) memset(dst[0], 0, bytes);
+    for (int i = exclusive; i < P; i++) memcpy(dst[i], in[0], bytes);
+    int rc = 0;
+    for (int pe = 1; pe < P; pe++)
+        for (int i = pe + exclusive; i < P; i++)
+            rc |= oracle_reduce_local(op, dt, (int) count, in[pe], dst[i]);
+    for (int p = 0; p < P; p++) free(in[p]);
+    free(in);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------
+ * Broadcast, src/collectives.c:429-485 (bcast_linear; bcast_tree :489-551 moves the
+ * same bytes): every non-root target receives the root's source.  The team forms
+ * (shmem_broadcastmem / shmem_<T>_broadcast, src/collectives_c.c4:380-429) also copy
+ * source to dest on the root; the active-set shmem_broadcast32/64 (:342-378) do not.
+ * ------------------------------------------------------------------------------ */
+int oracle_bcast(int P, size_t bytes, int root, int copy_root, void **src, void **dst)
+{
+    if (root < 0 || root >= P) return -3;
+    for (int p = 0; p < P; p++) {
+        if (p == root) {
+            if (copy_root && dst[p] != src[p]) memcpy(dst[p], src[p], bytes);
+        } else {
+            memcpy(dst[p], src[root], bytes);
+        }
+    }
+    return 0;
 }
 
 /* ------------------------------------------------------------------------------

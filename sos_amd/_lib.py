@@ -25,7 +25,14 @@ DTYPES = {
 }
 
 ORDER_LINEAR, ORDER_TREE = 0, 1
-ALGS = {"auto": 0, "recdbl": 1, "ring": 2, "rechalving": 3, "recdbl_direct": 4}
+ALGS = {"auto": 0, "recdbl": 1, "ring": 2, "rechalving": 3, "recdbl_direct": 4,
+        "inscan": 16, "exscan": 17}
+PLAN_INSCAN, PLAN_EXSCAN = 16, 17
+
+
+def plan_bcast(root, copy_root):
+    """Plan id of a broadcast from team index `root` (include/sosx.h SOSX_PLAN_BCAST)."""
+    return 32 + 2 * int(root) + (1 if copy_root else 0)
 DIST_UNIFORM, DIST_PROD = 0, 1
 
 ERRORS = {
@@ -58,6 +65,8 @@ _SIGS = {
                                  _c.c_size_t, _c.c_void_p]),
     "sosx_fold": (_c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
                              _c.POINTER(_c.c_void_p), _c.c_int, _c.c_size_t, _c.c_void_p]),
+    "sosx_prefix": (_c.c_int, [_c.c_int, _c.c_int, _c.POINTER(_c.c_void_p), _c.POINTER(_c.c_void_p),
+                               _c.c_int, _c.c_int, _c.c_size_t, _c.c_void_p]),
     "sosx_fill": (_c.c_int, [_c.c_int, _c.c_int, _c.c_uint64, _c.c_int, _c.c_void_p,
                              _c.c_size_t, _c.c_size_t, _c.c_void_p]),
     "sosx_count_mismatch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_size_t,
@@ -121,6 +130,15 @@ def fold(op, dtype, order, out_ptr, in_ptrs, count, stream=None):
     arr = (ctypes.c_void_p * len(in_ptrs))(*in_ptrs)
     return check(lib().sosx_fold(op_id(op), dtype_id(dtype), order, out_ptr, arr, len(in_ptrs),
                                  count, stream), "sosx_fold")
+
+
+def prefix(op, dtype, out_ptrs, in_ptrs, count, own=-1, stream=None):
+    """outs[k] = ins[0] OP ... OP ins[k] on device memory (sosx_prefix)."""
+    n = len(in_ptrs)
+    outs = (ctypes.c_void_p * n)(*out_ptrs)
+    ins = (ctypes.c_void_p * n)(*in_ptrs)
+    return check(lib().sosx_prefix(op_id(op), dtype_id(dtype), outs, ins, n, own, count, stream),
+                 "sosx_prefix")
 
 
 def fill(dtype, dist, seed, pe, dst_ptr, count, index0=0, stream=None):

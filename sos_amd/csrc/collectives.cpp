@@ -112,10 +112,22 @@ int run_locals(const sosplan::Round &r, const Bufs &b, int op, int dt, hipStream
             if (e != hipSuccess) return SOSX_ERR_HIP;
             continue;
         }
-        const void *ins[SOSX_MAX_FOLD];
+        if (l.kind == sosplan::ZERO) {
+            if (hipMemsetAsync(b.wat(l.out_buf, l.out_off), 0, l.count, stream) != hipSuccess)
+                return SOSX_ERR_HIP;
+            continue;
+        }
+        const void *ins[sosplan::PLAN_MAX_PE];
         for (int k = 0; k < l.nin; ++k) ins[k] = b.at(l.in_buf[k], l.in_off[k]);
         if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.fold_ev, g_prof.nf, false), stream);
-        int rc = sosx_fold(op, dt, l.order, b.wat(l.out_buf, l.out_off), ins, l.nin, l.count, stream);
+        int rc;
+        if (l.kind == sosplan::PREFIX) {
+            void *outs[sosplan::PLAN_MAX_PE];
+            for (int k = 0; k < l.nout; ++k) outs[k] = b.wat(l.outs_buf[k], l.outs_off[k]);
+            rc = sosx_prefix(op, dt, outs, ins, l.nin, l.own, l.count, stream);
+        } else {
+            rc = sosx_fold(op, dt, l.order, b.wat(l.out_buf, l.out_off), ins, l.nin, l.count, stream);
+        }
         if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.fold_ev, g_prof.nf, true), stream);
         if (rc) return rc;
     }
@@ -176,6 +188,87 @@ const char *status_text(int rc)
     }
 }
 
+// Run plan `alg` (a reduction SOSX_ALG_*, a scan or a broadcast, plan.h) for this PE
+// over team t, on the library stream; returns when the call is complete.
+void execute(int alg, void *target, const void *source, size_t count, size_t ts, const Team &t,
+             int op, int dt, const char *fn)
+{
+    State &s = st();
+    const size_t bytes = count * ts;
+    int rc;
+    if (s.transport == TRANSPORT_P2P) {
+        // buffers must live in the IPC-mapped device heap; anything else is staged
+        // through this PE's stage region (in place), whose offset is published
+        const char *hb = s.sym_stage;
+        auto in_heap = [&](const void *p) {
+            return hb && (const char *)p >= hb && (const char *)p + bytes <= hb + s.dev_heap_bytes;
+        };
+        const bool direct = in_heap(source) && in_heap(target);
+        const char *dsrc = (const char *)source;
+        char *ddst = (char *)target;
+        if (!direct) {
+            if (bytes > s.sym_stage_bytes)
+                raise_error("%s: %zu bytes outside the device symmetric heap exceed the p2p stage "
+                            "region (SHMEMX_STAGE_BYTES=%zu); allocate with shmemx_malloc_device",
+                            fn, bytes, s.sym_stage_bytes);
+            dsrc = ddst = s.sym_stage;
+        }
+        const unsigned smis = (unsigned)((uintptr_t)dsrc & 15), dmis = (unsigned)((uintptr_t)ddst & 15);
+        const Plan &p = cached_plan(alg, t.size, t.my_idx, count, ts, smis, dmis);
+        if (!direct && p.reads_src)
+            hip_check(hipMemcpyAsync(s.sym_stage, source, bytes, hipMemcpyDefault, s.stream), "stage in");
+        // scratch the peers read (scan results) lives in the stage region, after any
+        // staged operand; private scratch in the library's device buffer
+        char *scr = nullptr;
+        size_t scr_off = 0;
+        if (p.scratch_bytes && p.scr_sent) {
+            const size_t base = direct ? 0 : (bytes + 255) / 256 * 256;
+            if (base + p.scratch_bytes > s.sym_stage_bytes)
+                raise_error("%s: %zu bytes of exchange scratch exceed the p2p stage region "
+                            "(SHMEMX_STAGE_BYTES=%zu)", fn, (size_t)(base + p.scratch_bytes),
+                            s.sym_stage_bytes);
+            scr = s.sym_stage + base;
+            scr_off = base;
+        } else if (p.scratch_bytes) {
+            scr = (char *)scratch(p.scratch_bytes);
+        }
+        P2PBufs pb{dsrc, ddst, scr, (size_t)(dsrc - hb), (size_t)(ddst - hb), scr_off, smis, dmis};
+        if (g_prof.on) g_prof.ncall++;
+        rc = p2p_exec(p, t, alg, count, ts, pb, op, dt, s.stream);
+        if (rc) raise_error("%s: %s", fn, status_text(rc));
+        if (!direct && p.writes_dst)
+            hip_check(hipMemcpyAsync(target, s.sym_stage, bytes, hipMemcpyDefault, s.stream), "stage out");
+        hip_check(hipStreamSynchronize(s.stream), fn);
+        if (g_prof.on) g_prof.collect();
+        return;
+    }
+
+    // residency: device pointers run in place; host memory is staged through HBM
+    const bool dev_src = is_device_ptr(source);
+    const bool dev_dst = target == source ? dev_src : is_device_ptr(target);
+    const char *dsrc = (const char *)source;
+    char *ddst = (char *)target;
+    char *stg = nullptr;
+    const size_t half = (bytes + 255) / 256 * 256;
+    if (!dev_src || !dev_dst) {
+        stg = (char *)stage(2 * half);
+        if (!dev_src) dsrc = stg;
+        if (!dev_dst) ddst = target == source ? stg : stg + half;
+    }
+    const Plan &p = cached_plan(alg, t.size, t.my_idx, count, ts, (unsigned)((uintptr_t)dsrc & 15),
+                                (unsigned)((uintptr_t)ddst & 15));
+    if (!dev_src && p.reads_src)
+        hip_check(hipMemcpyAsync(stg, source, bytes, hipMemcpyHostToDevice, s.stream), "H2D");
+    Bufs b{dsrc, ddst, p.scratch_bytes ? (char *)scratch(p.scratch_bytes) : nullptr};
+    if (g_prof.on) g_prof.ncall++;
+    rc = exec_rccl(p, t, b, op, dt, s.stream);
+    if (rc) raise_error("%s: %s", fn, status_text(rc));
+    if (!dev_dst && p.writes_dst)
+        hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
+    hip_check(hipStreamSynchronize(s.stream), fn);
+    if (g_prof.on) g_prof.collect();
+}
+
 // shmem_internal_op_to_all for this PE over team t.
 void op_to_all(void *target, const void *source, size_t count, size_t ts, const Team &t, int op,
                int dt, const char *fn)
@@ -196,63 +289,7 @@ void op_to_all(void *target, const void *source, size_t count, size_t ts, const 
     int alg = sosplan::resolve_alg(s.reduce_alg, bytes, s.coll_size_crossover);
     if ((alg == SOSX_ALG_RING || alg == SOSX_ALG_RECDBL_DIRECT) && t.size > SOSX_MAX_FOLD)
         alg = SOSX_ALG_RECHALVING;
-
-    if (s.transport == TRANSPORT_P2P) {
-        // buffers must live in the IPC-mapped device heap; anything else is staged
-        // through this PE's stage region (in place), whose offset is published
-        const char *hb = s.sym_stage;
-        auto in_heap = [&](const void *p) {
-            return hb && (const char *)p >= hb && (const char *)p + bytes <= hb + s.dev_heap_bytes;
-        };
-        const bool direct = in_heap(source) && in_heap(target);
-        const char *dsrc = (const char *)source;
-        char *ddst = (char *)target;
-        if (!direct) {
-            if (bytes > s.sym_stage_bytes)
-                raise_error("%s: %zu bytes outside the device symmetric heap exceed the p2p stage "
-                            "region (SHMEMX_STAGE_BYTES=%zu); allocate with shmemx_malloc_device",
-                            fn, bytes, s.sym_stage_bytes);
-            hip_check(hipMemcpyAsync(s.sym_stage, source, bytes, hipMemcpyDefault, s.stream), "stage in");
-            dsrc = ddst = s.sym_stage;
-        }
-        const Plan &p = cached_plan(alg, t.size, t.my_idx, count, ts, (unsigned)((uintptr_t)dsrc & 15),
-                                    (unsigned)((uintptr_t)ddst & 15));
-        P2PBufs pb{dsrc, ddst, p.scratch_bytes ? (char *)scratch(p.scratch_bytes) : nullptr,
-                   (size_t)(dsrc - hb), (size_t)(ddst - hb)};
-        if (g_prof.on) g_prof.ncall++;
-        rc = p2p_exec(p, t, alg, count, ts, pb, op, dt, s.stream);
-        if (rc) raise_error("%s: %s", fn, status_text(rc));
-        if (!direct)
-            hip_check(hipMemcpyAsync(target, s.sym_stage, bytes, hipMemcpyDefault, s.stream), "stage out");
-        hip_check(hipStreamSynchronize(s.stream), fn);
-        if (g_prof.on) g_prof.collect();
-        return;
-    }
-
-    // residency: device pointers run in place; host memory is staged through HBM
-    const bool dev_src = is_device_ptr(source);
-    const bool dev_dst = target == source ? dev_src : is_device_ptr(target);
-    const char *dsrc = (const char *)source;
-    char *ddst = (char *)target;
-    if (!dev_src || !dev_dst) {
-        const size_t half = (bytes + 255) / 256 * 256;
-        char *stg = (char *)stage(2 * half);
-        if (!dev_src) {
-            hip_check(hipMemcpyAsync(stg, source, bytes, hipMemcpyHostToDevice, s.stream), "H2D");
-            dsrc = stg;
-        }
-        if (!dev_dst) ddst = target == source ? stg : stg + half;
-    }
-    const Plan &p = cached_plan(alg, t.size, t.my_idx, count, ts, (unsigned)((uintptr_t)dsrc & 15),
-                                (unsigned)((uintptr_t)ddst & 15));
-    Bufs b{dsrc, ddst, p.scratch_bytes ? (char *)scratch(p.scratch_bytes) : nullptr};
-    if (g_prof.on) g_prof.ncall++;
-    rc = exec_rccl(p, t, b, op, dt, s.stream);
-    if (rc) raise_error("%s: %s", fn, status_text(rc));
-    if (!dev_dst)
-        hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
-    hip_check(hipStreamSynchronize(s.stream), fn);
-    if (g_prof.on) g_prof.collect();
+    execute(alg, target, source, count, ts, t, op, dt, fn);
 }
 
 // SHMEM_ERR_CHECK_OVERLAP (src/shmem_internal.h:319-336), complete overlap allowed
@@ -324,6 +361,112 @@ int sos_api_reduce(shmem_team_t team, void *dest, const void *source, size_t nre
     return 0;
 }
 
+// Team-relative root check shared by the broadcasts (SHMEM_ERR_CHECK_PE, then the
+// root must be a member: src/collectives.c:435 real_root = PE_start + PE_root*stride).
+static void check_root(int PE_root, int size, const char *fn)
+{
+    if (PE_root < 0 || PE_root >= size)
+        raise_error("%s: Invalid PE_root %d (team/active set of %d PEs)", fn, PE_root, size);
+}
+
+int sos_api_broadcast(shmem_team_t team, void *dest, const void *source, size_t nelems,
+                      size_t type_size, int PE_root, const char *fn)
+{
+    check_initialized(fn);
+    Team *t = team_from_handle(team);
+    if (!t || !t->valid) raise_error("%s: invalid team", fn);
+    const size_t bytes = nelems * type_size;
+    check_symmetric(dest, bytes, "dest", fn);
+    check_symmetric(source, bytes, "source", fn);
+    check_overlap(dest, source, bytes, fn);
+    if (t->my_idx < 0) raise_error("%s: calling PE is not a member of the team", fn);
+    check_root(PE_root, t->size, fn);
+    if (bytes == 0) return 0;
+    // the team forms copy source to dest on the root as well (collectives_c.c4:390-397)
+    execute(sosplan::bcast_alg(PE_root, true), dest, source, nelems, type_size, *t, SOSX_OP_SUM,
+            SOSX_DT_UCHAR, fn);
+    return 0;
+}
+
+static void bcast_active_set(void *target, const void *source, size_t nlong, size_t ts,
+                             int PE_root, int PE_start, int logPE_stride, int PE_size, long *pSync,
+                             const char *fn)
+{
+    check_initialized(fn);
+    State &s = st();
+    const int stride = 1 << logPE_stride;
+    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) > s.n_pes)
+        raise_error("%s: Invalid active set (PE_start = %d, PE_stride = %d, PE_size = %d)", fn,
+                    PE_start, stride, PE_size);
+    if (!(s.my_pe >= PE_start && s.my_pe <= PE_start + ((PE_size - 1) * stride) &&
+          (s.my_pe - PE_start) % stride == 0))
+        raise_error("%s: Calling PE (%d) is not a member of the active set", fn, s.my_pe);
+    check_root(PE_root, PE_size, fn);
+    const size_t bytes = nlong * ts;
+    check_symmetric(target, bytes, "target", fn);
+    check_symmetric(source, bytes, "source", fn);
+    check_symmetric(pSync, sizeof(long) * SHMEM_BCAST_SYNC_SIZE, "pSync", fn);
+    check_overlap(target, source, bytes, fn);
+    if (PE_size == 1 || bytes == 0) return;  // src/collectives.c:441
+    Team t;
+    t.start = PE_start;
+    t.stride = stride;
+    t.size = PE_size;
+    t.my_idx = (s.my_pe - PE_start) / stride;
+    t.valid = true;
+    // the root's target is not written (collectives_c.c4:342-378)
+    execute(sosplan::bcast_alg(PE_root, false), target, source, nlong, ts, t, SOSX_OP_SUM,
+            SOSX_DT_UCHAR, fn);
+}
+
+void pshmem_broadcast32(void *target, const void *source, size_t nlong, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync)
+{
+    bcast_active_set(target, source, nlong, 4, PE_root, PE_start, logPE_stride, PE_size, pSync,
+                     "shmem_broadcast32");
+}
+
+void pshmem_broadcast64(void *target, const void *source, size_t nlong, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync)
+{
+    bcast_active_set(target, source, nlong, 8, PE_root, PE_start, logPE_stride, PE_size, pSync,
+                     "shmem_broadcast64");
+}
+
+int pshmem_broadcastmem(shmem_team_t team, void *dest, const void *source, size_t nelems,
+                        int PE_root)
+{
+    return sos_api_broadcast(team, dest, source, nelems, 1, PE_root, "shmem_broadcastmem");
+}
+
+void shmem_broadcast32(void *, const void *, size_t, int, int, int, int, long *)
+    __attribute__((weak, alias("pshmem_broadcast32")));
+void shmem_broadcast64(void *, const void *, size_t, int, int, int, int, long *)
+    __attribute__((weak, alias("pshmem_broadcast64")));
+int shmem_broadcastmem(shmem_team_t, void *, const void *, size_t, int)
+    __attribute__((weak, alias("pshmem_broadcastmem")));
+
+int sos_api_scan(shmem_team_t team, void *dest, const void *source, size_t nelems,
+                 size_t type_size, int op, int datatype, int exclusive, const char *fn)
+{
+    check_initialized(fn);
+    Team *t = team_from_handle(team);
+    if (!t || !t->valid) raise_error("%s: invalid team", fn);
+    const size_t bytes = nelems * type_size;
+    check_symmetric(dest, bytes, "dest", fn);
+    check_symmetric(source, bytes, "source", fn);
+    check_overlap(dest, source, bytes, fn);
+    if (t->my_idx < 0) raise_error("%s: calling PE is not a member of the team", fn);
+    if (nelems == 0) return 0;
+    int rc = sos_check_op(op, datatype);
+    if (rc) raise_error("%s: %s (datatype %d, op %d)", fn, status_text(rc), datatype, op);
+    if (t->size > sosplan::PLAN_MAX_PE)
+        raise_error("%s: teams of more than %d PEs are not supported", fn, sosplan::PLAN_MAX_PE);
+    execute(exclusive ? sosplan::PLAN_EXSCAN : sosplan::PLAN_INSCAN, dest, source, nelems,
+            type_size, *t, op, datatype, fn);
+    return 0;
+}
+
 int shmemx_reduce_local(int op, int datatype, size_t count, const void *in, void *inout)
 {
     check_initialized("shmemx_reduce_local");
@@ -355,8 +498,10 @@ int sosx_loopback_allreduce(int alg, int P, int op, int datatype, void *const *s
                             void *const *dsts, size_t count, void *stream)
 {
     if (P < 1 || P > SOSX_MAX_FOLD || !srcs || !dsts) return SOSX_ERR_ARG;
-    int rc = sos_check_op(op, datatype);
+    int rc = sosplan::is_bcast(alg) ? (sos_dtype_info(datatype).size ? SOSX_OK : SOSX_ERR_DTYPE)
+                                    : sos_check_op(op, datatype);
     if (rc) return rc;
+    if (sosplan::is_bcast(alg) && ((alg - sosplan::PLAN_BCAST) >> 1) >= P) return SOSX_ERR_ARG;
     const size_t ts = sos_dtype_info(datatype).size;
     hipStream_t sm = (hipStream_t)stream;
     const int a = sosplan::resolve_alg(alg, count * ts, 16384);

@@ -49,12 +49,11 @@ template <class F> __device__ __forceinline__ F csign(F m, F s)
 // x86 SSE NaN rule for `first + second` (Intel SDM vol.1 table 4-7): a NaN first
 // operand wins, else a NaN second operand, both returned quieted; an invalid operation
 // on non-NaN inputs returns the default NaN (sign set: 0xFFC00000 / 0xFFF8...).
-template <class F> __device__ __forceinline__ F x86_add(F first, F second)
+template <class F> __device__ __forceinline__ F x86_nan(F r, F first, F second)
 {
     using I = typename std::conditional<sizeof(F) == 4, uint32_t, uint64_t>::type;
     constexpr I qbit = sizeof(F) == 4 ? (I)0x00400000u : (I)0x0008000000000000ull;
     constexpr I dnan = sizeof(F) == 4 ? (I)0xFFC00000u : (I)0xFFF8000000000000ull;
-    F r = first + second;
     if (__builtin_isnan(r)) {
         I bits = __builtin_isnan(first)    ? (__builtin_bit_cast(I, first) | qbit)
                  : __builtin_isnan(second) ? (__builtin_bit_cast(I, second) | qbit)
@@ -62,6 +61,14 @@ template <class F> __device__ __forceinline__ F x86_add(F first, F second)
         r = __builtin_bit_cast(F, bits);
     }
     return r;
+}
+template <class F> __device__ __forceinline__ F x86_add(F first, F second)
+{
+    return x86_nan(first + second, first, second);
+}
+template <class F> __device__ __forceinline__ F x86_mul(F first, F second)
+{
+    return x86_nan(first * second, first, second);
 }
 
 template <class F>
@@ -137,7 +144,9 @@ struct OpSum {
             using U = typename std::make_unsigned<W>::type;
             return (T)((U)a + (U)b);
         } else {
-            return a + b;
+            // gcc -O2: `addss in, out` -- the inout operand is SSE's first operand, whose
+            // NaN wins; hipcc may commute a plain fadd, so the rule is explicit
+            return x86_add(a, b);
         }
     }
     // gcc -O2 (x86-64) emits `addss in.re -> out.re` and `addss out.im -> in.im` for the
@@ -162,7 +171,7 @@ struct OpProd {
             using U = typename std::make_unsigned<W>::type;
             return (T)((U)a * (U)b);
         } else {
-            return a * b;
+            return x86_mul(a, b);  // `mulss in, out`: first-operand NaN rule as for sum
         }
     }
     __device__ __forceinline__ static cf32 f(cf32 a, cf32 b)

@@ -7,7 +7,8 @@
 //   LINEAR: acc = in[0]; acc = acc OP in[k]  -- the ring reduce-scatter fold
 //           (src/collectives.c:693-727: partial = partial OP own source);
 //   TREE  : the recdbl_sw butterfly (src/collectives.c:905-963).
-// P <= 8 (one PE per GPU on one node) and is a template parameter.
+// P <= 8 (one PE per GPU on one node) is a template parameter; 9..64 run a runtime-P
+// element loop.
 #include "elementwise.h"
 
 namespace sos {
@@ -112,6 +113,114 @@ __global__ __launch_bounds__(kThreads) void k_fold_scalar(T *__restrict__ out, F
     }
 }
 
+// Runtime P (9..64 PEs per team: several PEs per GPU or more than one node): element
+// loads; the TREE order walks the recdbl_sw leaves left to right with a binary-counter
+// stack (merge equal-height neighbours: w[k] = w[k] OP w[k+d]), so no P-sized array.
+template <class T, class OP, int ORDER>
+__global__ __launch_bounds__(kThreads) void k_fold_dyn(T *__restrict__ out, FoldPtrs ins, int np,
+                                                         size_t n)
+{
+    const size_t stride = (size_t)gridDim.x * kThreads;
+    int p2 = 1;
+    while (p2 * 2 <= np) p2 *= 2;
+    for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+        if constexpr (ORDER == SOSX_ORDER_LINEAR) {
+            T acc = ((const T *)ins.p[0])[i];
+            for (int k = 1; k < np; ++k) acc = OP::f(acc, ((const T *)ins.p[k])[i]);
+            out[i] = acc;
+        } else {
+            T val[8];
+            int height[8];
+            int top = 0;
+            for (int k = 0; k < p2; ++k) {
+                T leaf = ((const T *)ins.p[k])[i];
+                if (k < np - p2) leaf = OP::f(leaf, ((const T *)ins.p[k + p2])[i]);
+                val[top] = leaf;
+                height[top] = 0;
+                ++top;
+                while (top >= 2 && height[top - 1] == height[top - 2]) {
+                    val[top - 2] = OP::f(val[top - 2], val[top - 1]);
+                    height[top - 2]++;
+                    --top;
+                }
+            }
+            out[i] = val[0];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Fused prefix (the team scan's local step): outs[k] = ins[0] OP ... OP ins[k].
+// P inputs, P outputs, one pass: 2*P*n*s HBM bytes.  NP <= 8: every input of a vector
+// is loaded before the first store (any output may alias any input).  Larger P: a
+// runtime loop; the one input that may alias an output (`own`, the PE's own source
+// chunk under an in-place scan) is loaded before any store.
+// ---------------------------------------------------------------------------------
+constexpr int kMaxPrefix = 64;
+
+struct PrefixPtrs {
+    const void *in[kMaxPrefix];
+    void *out[kMaxPrefix];
+};
+
+template <class T, class OP, int NP>
+__global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        u32x4 x[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            x[k] = ldv<true>(reinterpret_cast<const u32x4 *>((const T *)p.in[k] + g.head) + i);
+        u32x4 acc = x[0];
+        stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[0] + g.head) + i, acc);
+#pragma unroll
+        for (int k = 1; k < NP; ++k) {
+            acc = apply<T, OP>(acc, x[k]);
+            stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[k] + g.head) + i, acc);
+        }
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)p.in[k])[i];
+            T acc = v[0];
+            ((T *)p.out[0])[i] = acc;
+#pragma unroll
+            for (int k = 1; k < NP; ++k) {
+                acc = OP::f(acc, v[k]);
+                ((T *)p.out[k])[i] = acc;
+            }
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
+template <class T, class OP>
+__device__ __forceinline__ void prefix_elem_dyn(const PrefixPtrs &p, int np, int own, size_t i)
+{
+    const T ov = own >= 0 ? ((const T *)p.in[own])[i] : T();
+    T acc = own == 0 ? ov : ((const T *)p.in[0])[i];
+    ((T *)p.out[0])[i] = acc;
+    for (int k = 1; k < np; ++k) {
+        acc = OP::f(acc, k == own ? ov : ((const T *)p.in[k])[i]);
+        ((T *)p.out[k])[i] = acc;
+    }
+}
+
+// Runtime P (any P <= 64, or 16-B incongruent operands): element loads.
+template <class T, class OP>
+__global__ __launch_bounds__(kThreads) void k_prefix_dyn(PrefixPtrs p, int np, int own, size_t n)
+{
+    const size_t stride = (size_t)gridDim.x * kThreads;
+    for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
+        prefix_elem_dyn<T, OP>(p, np, own, i);
+}
+
 }  // namespace sos
 
 using namespace sos;
@@ -149,7 +258,13 @@ int launch_fold(T *out, const FoldPtrs &ins, int nin, size_t n, hipStream_t st)
         case 6: return launch_fold_np<T, OP, 6, ORDER>(out, ins, n, st);
         case 7: return launch_fold_np<T, OP, 7, ORDER>(out, ins, n, st);
         case 8: return launch_fold_np<T, OP, 8, ORDER>(out, ins, n, st);
-        default: return SOSX_ERR_ARG;
+        default: {
+            size_t blocks = (n + kThreads - 1) / kThreads;
+            if (blocks > 8192) blocks = 8192;
+            hipLaunchKernelGGL((k_fold_dyn<T, OP, ORDER>), dim3((unsigned)blocks), dim3(kThreads), 0,
+                               st, out, ins, nin, n);
+            return hip_ok(hipGetLastError());
+        }
     }
 }
 
@@ -162,9 +277,67 @@ struct FoldFn {
     }
 };
 
+template <class T, class OP, int NP>
+int launch_prefix_np(const PrefixPtrs &p, size_t n, hipStream_t st)
+{
+    const uintptr_t o = (uintptr_t)p.out[0];
+    Geom g = make_geom(o, n, sizeof(T), 1);
+    hipLaunchKernelGGL((k_prefix<T, OP, NP>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st, p, g);
+    return hip_ok(hipGetLastError());
+}
+
+struct PrefixFn {
+    template <class T, class OP>
+    static int run(const PrefixPtrs *p, int np, int own, size_t n, hipStream_t st)
+    {
+        const uintptr_t o = (uintptr_t)p->out[0];
+        bool congruent = (o % sizeof(T)) == 0 && sizeof(T) <= 16;
+        for (int k = 0; k < np; ++k)
+            congruent &= (((uintptr_t)p->in[k] ^ o) & 15) == 0 && (((uintptr_t)p->out[k] ^ o) & 15) == 0;
+        if (congruent) {
+            switch (np) {
+                case 1: return launch_prefix_np<T, OP, 1>(*p, n, st);
+                case 2: return launch_prefix_np<T, OP, 2>(*p, n, st);
+                case 3: return launch_prefix_np<T, OP, 3>(*p, n, st);
+                case 4: return launch_prefix_np<T, OP, 4>(*p, n, st);
+                case 5: return launch_prefix_np<T, OP, 5>(*p, n, st);
+                case 6: return launch_prefix_np<T, OP, 6>(*p, n, st);
+                case 7: return launch_prefix_np<T, OP, 7>(*p, n, st);
+                case 8: return launch_prefix_np<T, OP, 8>(*p, n, st);
+                default: break;
+            }
+        }
+        size_t blocks = (n + kThreads - 1) / kThreads;
+        if (blocks > 8192) blocks = 8192;
+        hipLaunchKernelGGL((k_prefix_dyn<T, OP>), dim3((unsigned)blocks), dim3(kThreads), 0, st, *p,
+                           np, own, n);
+        return hip_ok(hipGetLastError());
+    }
+};
+
 }  // namespace
 
 extern "C" {
+
+// outs[k] = ins[0] OP ins[1] OP ... OP ins[k] (left operand the running prefix), k < np,
+// np <= 64.  `own` (or -1) names the one input that may alias an output when np > 8.
+int sosx_prefix(int op, int dtype, void *const *outs, const void *const *ins, int np, int own,
+                size_t count, void *stream)
+{
+    if (np < 1 || np > kMaxPrefix || own >= np) return SOSX_ERR_ARG;
+    int rc = sos_check_op(op, dtype);
+    if (rc) return rc;
+    if (count == 0) return SOSX_OK;
+    if (!outs || !ins) return SOSX_ERR_ARG;
+    PrefixPtrs pp;
+    memset(&pp, 0, sizeof(pp));
+    for (int k = 0; k < np; ++k) {
+        if (!outs[k] || !ins[k]) return SOSX_ERR_ARG;
+        pp.in[k] = ins[k];
+        pp.out[k] = outs[k];
+    }
+    return dispatch<PrefixFn>(op, dtype, &pp, np, own, count, as_stream(stream));
+}
 
 int sosx_fold(int op, int dtype, int order, void *out, const void *const *ins, int nin,
               size_t count, void *stream)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generate the typed SOS reduction entry points.
+"""Generate the typed SOS reduction / scan / broadcast entry points.
 
 SOS stamps its reductions out of m4 type tables (bindings/shmem_bind_c.m4:93-180)
 through SHMEM_DEF_TO_ALL / SHMEM_DEF_REDUCE (src/collectives_c.c4:221-292).  This
@@ -9,9 +9,14 @@ makes their min/max compare signed -- and writes:
 
   include/shmem_reductions.h      198 prototypes + C11 _Generic macros
                                   (mpp/shmem.h4:952-991) + C++ overloads (:249-296)
-  sos_amd/csrc/reductions_gen.cpp 198 definitions (strong pshmem_*, weak shmem_*
+  include/shmemx_scans.h          52 shmemx_<T>_sum_{inscan,exscan} prototypes + generics
+                                  (mpp/shmemx_c_func.h4:78-86, mpp/shmemx.h4:71-133)
+  sos_amd/csrc/reductions_gen.cpp the definitions (strong pshmem_*, weak shmem_*
                                   aliases as SOS's profiling interface,
-                                  src/collectives_c.c4:36-166)
+                                  src/collectives_c.c4:36-166), plus the 24 typed team
+                                  broadcasts shmem_<T>_broadcast (SHMEM_BIND_C_RMA,
+                                  src/collectives_c.c4:402-429) and the 52 scans
+                                  (src/collectives_c.c4:294-340)
 
 Run: python sos_amd/csrc/gen_bindings.py   (build() runs it; output is committed).
 """
@@ -47,6 +52,16 @@ MIN_MAX = [
     ("longdouble", "long double", "LONG_DOUBLE")]
 SUM_PROD = MIN_MAX + [("complexd", "double _Complex", "DOUBLE_COMPLEX"),
                       ("complexf", "float _Complex", "FLOAT_COMPLEX")]
+# bindings/shmem_bind_c.m4:10-34 (broadcast element types; bytes only, no ITYPE)
+RMA = [("float", "float"), ("double", "double"), ("longdouble", "long double"), ("char", "char"),
+       ("schar", "signed char"), ("short", "short"), ("int", "int"), ("long", "long"),
+       ("longlong", "long long"), ("uchar", "unsigned char"), ("ushort", "unsigned short"),
+       ("uint", "unsigned int"), ("ulong", "unsigned long"), ("ulonglong", "unsigned long long"),
+       ("int8", "int8_t"), ("int16", "int16_t"), ("int32", "int32_t"), ("int64", "int64_t"),
+       ("uint8", "uint8_t"), ("uint16", "uint16_t"), ("uint32", "uint32_t"), ("uint64", "uint64_t"),
+       ("size", "size_t"), ("ptrdiff", "ptrdiff_t")]
+# bindings/shmem_bind_c11.m4:13-28 (generic selector: base types only)
+GENERIC_RMA = RMA[:14]
 FLOATS = [("float", "float", "FLOAT"), ("double", "double", "DOUBLE"),
           ("longdouble", "long double", "LONG_DOUBLE")]
 CMPLX = [("complexf", "float _Complex", "FLOAT_COMPLEX"),
@@ -96,12 +111,66 @@ def reduce_sig(prefix, st, ct, op):
             f"size_t nreduce)")
 
 
+def bcast_sig(prefix, st, ct):
+    return (f"int {prefix}shmem_{st}_broadcast(shmem_team_t team, {ct} *dest, const {ct} *source, "
+            f"size_t nelems, int PE_root)")
+
+
+def scan_sig(prefix, st, ct, kind):
+    return (f"int {prefix}shmemx_{st}_sum_{kind}(shmem_team_t team, {ct} *dest, const {ct} *source, "
+            f"size_t nelems)")
+
+
+SCANS = [(t, k) for k in ("exscan", "inscan") for t in SUM_PROD]
+
+
+def c11_generic(name, arms, argidx=1):
+    out = [f"#define {name}(...) \\",
+           f"    _Generic(SHMEM_C11_TYPE_EVAL_PTR(SHMEM_C11_ARG{argidx}(__VA_ARGS__)), \\",
+           ", \\\n".join(arms) + " \\", "    )(__VA_ARGS__)"]
+    return out
+
+
+def scan_header():
+    out = ["/* shmemx_scans.h -- GENERATED by sos_amd/csrc/gen_bindings.py; do not edit.",
+           " *",
+           " * SOS's team prefix-sum extensions shmemx_<T>_sum_{inscan,exscan}",
+           " * (mpp/shmemx_c_func.h4:78-86) with their C++ overloads and C11 generic",
+           " * selectors (mpp/shmemx.h4:71-133). */",
+           "#ifndef SHMEMX_SCANS_H", "#define SHMEMX_SCANS_H", "",
+           "#ifdef __cplusplus", 'extern "C" {', "#endif", ""]
+    for (st, ct, it), k in SCANS:
+        out.append(f"SHMEM_FUNCTION_ATTRIBUTES {scan_sig('', st, ct, k)};")
+    for (st, ct, it), k in SCANS:
+        out.append(f"{scan_sig('p', st, ct, k)};")
+    out += ["", "#ifdef __cplusplus", "}  /* extern \"C\" */", "#endif", ""]
+    out.append("#if defined(__cplusplus)")
+    for k in ("exscan", "inscan"):
+        for st, ct in GENERIC_TABLE["sum"]:
+            out.append(f"static inline int shmemx_sum_{k}(shmem_team_t team, {ct} *dest, "
+                       f"const {ct} *source, size_t nelems) {{ return shmemx_{st}_sum_{k}(team, "
+                       f"dest, source, nelems); }}")
+    out.append("#elif defined(__STDC_VERSION__) && __STDC_VERSION__ >= 201112L")
+    out.append("#ifndef SHMEM_C11_TYPE_EVAL_PTR")
+    out.append("#define SHMEM_C11_TYPE_EVAL_PTR(arg) &*(arg)")
+    out.append("#define SHMEM_C11_ARG1(first, ...) SHMEM_C11_ARG1_HELPER(__VA_ARGS__, sentinel)")
+    out.append("#define SHMEM_C11_ARG1_HELPER(second, ...) second")
+    out.append("#endif")
+    for k in ("exscan", "inscan"):
+        out += c11_generic(f"shmemx_sum_{k}",
+                           [f"        {ct}*: shmemx_{st}_sum_{k}" for st, ct in GENERIC_TABLE["sum"]])
+    out.append("#endif")
+    out += ["", "#endif /* SHMEMX_SCANS_H */", ""]
+    return "\n".join(out)
+
+
 def header():
     out = ["/* shmem_reductions.h -- GENERATED by sos_amd/csrc/gen_bindings.py; do not edit.",
            " *",
            " * The SOS reduction family: 44 active-set *_to_all and 154 team *_reduce entry",
-           " * points with SOS's signatures (mpp/shmem_c_func.h4:413-438, :688-702), the C11",
-           " * generic selectors (mpp/shmem.h4:952-991) and C++ overloads (:249-296). */",
+           " * points with SOS's signatures (mpp/shmem_c_func.h4:413-438, :688-702), the 24",
+           " * typed team broadcasts (:673-676), the C11 generic selectors (mpp/shmem.h4:",
+           " * 934-939, :952-991) and C++ overloads (:228-233, :249-296). */",
            "#ifndef SHMEM_REDUCTIONS_H", "#define SHMEM_REDUCTIONS_H", "",
            "#ifdef __cplusplus", 'extern "C" {', "#endif", ""]
     out.append("/* active-set reductions (deprecated in OpenSHMEM 1.5, kept by SOS) */")
@@ -112,11 +181,17 @@ def header():
     for (st, ct, it), op in REDUCE:
         out.append(f"SHMEM_FUNCTION_ATTRIBUTES {reduce_sig('', st, ct, op)};")
     out.append("")
+    out.append("/* typed team broadcasts (mpp/shmem_c_func.h4:673-676) */")
+    for st, ct in RMA:
+        out.append(f"SHMEM_FUNCTION_ATTRIBUTES {bcast_sig('', st, ct)};")
+    out.append("")
     out.append("/* profiling interface: pshmem_* are the implementations, shmem_* weak aliases */")
     for (st, ct, it), op in TO_ALL:
         out.append(f"{to_all_sig('p', st, ct, op)};")
     for (st, ct, it), op in REDUCE:
         out.append(f"{reduce_sig('p', st, ct, op)};")
+    for st, ct in RMA:
+        out.append(f"{bcast_sig('p', st, ct)};")
     out += ["", "#ifdef __cplusplus", "}  /* extern \"C\" */", "#endif", ""]
     # C++ overloads
     out.append("#if defined(__cplusplus)")
@@ -125,6 +200,10 @@ def header():
             out.append(f"static inline int shmem_{op}_reduce(shmem_team_t team, {ct} *dest, "
                        f"const {ct} *source, size_t nreduce) {{ return shmem_{st}_{op}_reduce(team, "
                        f"dest, source, nreduce); }}")
+    for st, ct in GENERIC_RMA:
+        out.append(f"static inline int shmem_broadcast(shmem_team_t team, {ct} *dest, const {ct} *source, "
+                   f"size_t nelems, int PE_root) {{ return shmem_{st}_broadcast(team, dest, source, "
+                   f"nelems, PE_root); }}")
     # C11 generics
     out.append("#elif defined(__STDC_VERSION__) && __STDC_VERSION__ >= 201112L")
     out.append("#define SHMEM_C11_TYPE_EVAL_PTR(arg) &*(arg)")
@@ -136,6 +215,7 @@ def header():
         out.append("    _Generic(SHMEM_C11_TYPE_EVAL_PTR(SHMEM_C11_ARG1(__VA_ARGS__)), \\")
         out.append(", \\\n".join(arms) + " \\")
         out.append("    )(__VA_ARGS__)")
+    out += c11_generic("shmem_broadcast", [f"        {ct}*: shmem_{st}_broadcast" for st, ct in GENERIC_RMA])
     out.append("#endif")
     out += ["", "#endif /* SHMEM_REDUCTIONS_H */", ""]
     return "\n".join(out)
@@ -147,7 +227,8 @@ def source():
            "// The 198 typed SOS reduction entry points.  Each is SHMEM_DEF_TO_ALL or",
            "// SHMEM_DEF_REDUCE (src/collectives_c.c4:221-269): argument checks, then the",
            "// dispatcher with the (op, internal datatype) pair of bindings/shmem_bind_c.m4.",
-           '#include "shmem.h"', '#include "sosx.h"', '#include "api_internal.h"', "",
+           '#include "shmem.h"', '#include "shmemx.h"', '#include "sosx.h"',
+           '#include "api_internal.h"', "",
            'extern "C" {', ""]
     for (st, ct, it), op in TO_ALL:
         name = f"shmem_{st}_{op}_to_all"
@@ -167,19 +248,41 @@ def source():
         out.append("}")
         out.append(f"{reduce_sig('', st, ct, op)} __attribute__((weak, alias(\"p{name}\")));")
         out.append("")
+    for st, ct in RMA:
+        name = f"shmem_{st}_broadcast"
+        out.append(f"{bcast_sig('p', st, ct)}")
+        out.append("{")
+        out.append(f"    return sos_api_broadcast(team, dest, source, nelems, sizeof({ct}), PE_root, "
+                   f"\"{name}\");")
+        out.append("}")
+        out.append(f"{bcast_sig('', st, ct)} __attribute__((weak, alias(\"p{name}\")));")
+        out.append("")
+    for (st, ct, it), k in SCANS:
+        name = f"shmemx_{st}_sum_{k}"
+        out.append(f"{scan_sig('p', st, ct, k)}")
+        out.append("{")
+        out.append(f"    return sos_api_scan(team, dest, source, nelems, sizeof({ct}), SOSX_OP_SUM, "
+                   f"SOSX_DT_{it}, {1 if k == 'exscan' else 0}, \"{name}\");")
+        out.append("}")
+        out.append(f"{scan_sig('', st, ct, k)} __attribute__((weak, alias(\"p{name}\")));")
+        out.append("")
     out += ['}  // extern "C"', ""]
     return "\n".join(out)
 
 
 def symbols():
-    """All 198 public names (used by the ABI test)."""
+    """All generated public names (used by the ABI test)."""
     return ([f"shmem_{st}_{op}_to_all" for (st, ct, it), op in TO_ALL]
-            + [f"shmem_{st}_{op}_reduce" for (st, ct, it), op in REDUCE])
+            + [f"shmem_{st}_{op}_reduce" for (st, ct, it), op in REDUCE]
+            + [f"shmem_{st}_broadcast" for st, ct in RMA]
+            + [f"shmemx_{st}_sum_{k}" for (st, ct, it), k in SCANS])
 
 
 def main():
     assert len(TO_ALL) == 44 and len(REDUCE) == 154, (len(TO_ALL), len(REDUCE))
+    assert len(RMA) == 24 and len(SCANS) == 52, (len(RMA), len(SCANS))
     targets = {os.path.join(ROOT, "include", "shmem_reductions.h"): header(),
+               os.path.join(ROOT, "include", "shmemx_scans.h"): scan_header(),
                os.path.join(ROOT, "sos_amd", "csrc", "reductions_gen.cpp"): source()}
     check = "--check" in sys.argv
     stale = False

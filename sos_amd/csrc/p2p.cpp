@@ -35,6 +35,8 @@
 #include "runtime.h"
 #include "sosx.h"
 
+extern "C" int sosx_prefix(int op, int dtype, void *const *outs, const void *const *ins, int np,
+                           int own, size_t count, void *stream);
 extern "C" int sosx_gather(int nseg, const void *const *srcs, void *const *dsts,
                            const size_t *bytes, void *stream);
 
@@ -50,8 +52,11 @@ struct P2PShared {
     std::atomic<uint64_t> posted[kMaxPE][kMaxPE];
     std::atomic<uint64_t> consumed[kMaxPE][kMaxPE];
     struct Pub {
-        std::atomic<uint64_t> src_off, dst_off;
+        std::atomic<uint64_t> src_off, dst_off, scr_off, mis;
     } pub[kMaxPE];
+    // team creation agreement (runtime.cpp shmem_team_split_strided): per world PE, the
+    // free team-slot bit mask and the creation status, read by the other members
+    std::atomic<uint64_t> team_word[2][kMaxPE];
 };
 
 // What this PE has seen/done per ordered pair (monotonic across calls).
@@ -85,17 +90,19 @@ struct PeerSend {
     uint64_t off, bytes;
 };
 
-// The sends peer q's plan makes to `me`, in order (deterministic: rebuild q's plan).
+// The sends peer q's plan makes to `me`, in order (deterministic: rebuild q's plan from
+// its published operand misalignment, which places its scratch slots).
 const std::vector<PeerSend> &peer_sends(int alg, int P, int q, int me, uint64_t count,
-                                        uint64_t ts)
+                                        uint64_t ts, uint64_t mis)
 {
-    static std::map<std::tuple<int, int, int, int, uint64_t, uint64_t>, std::vector<PeerSend>> cache;
-    auto key = std::make_tuple(alg, P, q, me, count, ts);
+    static std::map<std::tuple<int, int, int, int, uint64_t, uint64_t, uint64_t>,
+                    std::vector<PeerSend>> cache;
+    auto key = std::make_tuple(alg, P, q, me, count, ts, mis);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
     if (cache.size() > 512) cache.clear();
     sosplan::Plan p;
-    if (sosplan::build(alg, P, q, count, ts, 0, 0, &p) != SOSX_OK)
+    if (sosplan::build(alg, P, q, count, ts, (unsigned)(mis & 15), (unsigned)(mis >> 4), &p) != SOSX_OK)
         raise_error("p2p transport: cannot build the plan of PE %d", q);
     std::vector<PeerSend> v;
     for (const auto &r : p.rounds)
@@ -113,6 +120,16 @@ bool overlaps(const char *a, uint64_t na, const char *b, uint64_t nb)
 
 size_t p2p_shared_bytes() { return sizeof(P2PShared); }
 
+void team_word_put(int which, int world_pe, uint64_t v)
+{
+    shared()->team_word[which][world_pe].store(v, std::memory_order_release);
+}
+
+uint64_t team_word_get(int which, int world_pe)
+{
+    return shared()->team_word[which][world_pe].load(std::memory_order_acquire);
+}
+
 int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, uint64_t ts,
              const P2PBufs &b, int op, int dt, hipStream_t stream)
 {
@@ -122,6 +139,9 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
     const int me = t.my_idx;
     const int my_world = t.world_rank(me);
     sh->pub[my_world].src_off.store(b.src_off, std::memory_order_relaxed);
+    sh->pub[my_world].scr_off.store(b.scr_off, std::memory_order_relaxed);
+    sh->pub[my_world].mis.store((uint64_t)(b.smis & 15) | (uint64_t)(b.dmis & 15) << 4,
+                                std::memory_order_relaxed);
     sh->pub[my_world].dst_off.store(b.dst_off, std::memory_order_release);
     std::vector<int> recv_idx((size_t)t.size, 0);  // k-th receive from each team peer
     auto local_ptr = [&](int buf, uint64_t off) -> char * {
@@ -148,31 +168,38 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
             const int pw = t.world_rank(x.peer);
             const uint64_t want = ++g_local.seen_from[pw];
             spin_until(sh->posted[pw][my_world], want, "a peer's data");
-            const auto &sends = peer_sends(alg, t.size, x.peer, me, count, ts);
+            const uint64_t dst_off = sh->pub[pw].dst_off.load(std::memory_order_acquire);
+            const auto &sends = peer_sends(alg, t.size, x.peer, me, count, ts,
+                                           sh->pub[pw].mis.load(std::memory_order_relaxed));
             const int k = recv_idx[(size_t)x.peer]++;
             if (k >= (int)sends.size() || sends[(size_t)k].bytes != x.bytes)
                 raise_error("p2p transport: plan mismatch with PE %d", pw);
             const PeerSend &ps = sends[(size_t)k];
-            const uint64_t boff = ps.buf == sosplan::SRC
-                ? sh->pub[pw].src_off.load(std::memory_order_acquire)
-                : sh->pub[pw].dst_off.load(std::memory_order_acquire);
+            const uint64_t boff = ps.buf == sosplan::SRC ? sh->pub[pw].src_off.load(std::memory_order_relaxed)
+                                : ps.buf == sosplan::DST ? dst_off
+                                                         : sh->pub[pw].scr_off.load(std::memory_order_relaxed);
             const char *remote = s.peer_heap[(size_t)pw] + boff + ps.off;
             segs.push_back(Seg{remote, local_ptr(x.buf, x.off), x.bytes, pw, false});
         }
-        // 3. folds read received chunks in place when no output overlaps a send
+        // 3. folds/prefixes read received chunks in place when no output overlaps a send
         bool fuse_ok = true;
         for (const auto &l : r.ops) {
-            const uint64_t ob = l.kind == sosplan::FOLD ? l.count * ts : l.count;
-            for (const auto &x : r.xfers)
-                if (x.send && overlaps(local_ptr(l.out_buf, l.out_off), ob, local_ptr(x.buf, x.off), x.bytes))
-                    fuse_ok = false;
+            const bool typed = l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX;
+            const uint64_t ob = typed ? l.count * ts : l.count;
+            const int nout = l.kind == sosplan::PREFIX ? l.nout : 1;
+            for (int k = 0; k < nout; ++k) {
+                const char *o = l.kind == sosplan::PREFIX ? local_ptr(l.outs_buf[k], l.outs_off[k])
+                                                          : local_ptr(l.out_buf, l.out_off);
+                for (const auto &x : r.xfers)
+                    if (x.send && overlaps(o, ob, local_ptr(x.buf, x.off), x.bytes)) fuse_ok = false;
+            }
         }
         std::vector<std::vector<const void *>> fold_ins(r.ops.size());
         for (size_t i = 0; i < r.ops.size(); ++i) {
             const auto &l = r.ops[i];
             for (int k = 0; k < l.nin; ++k) {
                 const char *p = local_ptr(l.in_buf[k], l.in_off[k]);
-                if (fuse_ok && l.kind == sosplan::FOLD)
+                if (fuse_ok && (l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX))
                     for (auto &sg : segs)
                         if (sg.dst == p && sg.bytes == l.count * ts) {
                             p = sg.src;
@@ -204,6 +231,20 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
                         hipMemcpyAsync(local_ptr(l.out_buf, l.out_off), fold_ins[i][0], l.count,
                                        hipMemcpyDeviceToDevice, stream) != hipSuccess)
                         return SOSX_ERR_HIP;
+                    continue;
+                }
+                if (l.kind == sosplan::ZERO) {
+                    if (hipMemsetAsync(local_ptr(l.out_buf, l.out_off), 0, l.count, stream) != hipSuccess)
+                        return SOSX_ERR_HIP;
+                    continue;
+                }
+                if (l.kind == sosplan::PREFIX) {
+                    void *outs[sosplan::PLAN_MAX_PE];
+                    for (int k = 0; k < l.nout; ++k) outs[k] = local_ptr(l.outs_buf[k], l.outs_off[k]);
+                    prof_mark(0, false, stream);
+                    int rc = sosx_prefix(op, dt, outs, fold_ins[i].data(), l.nin, l.own, l.count, stream);
+                    prof_mark(0, true, stream);
+                    if (rc) return rc;
                     continue;
                 }
                 prof_mark(0, false, stream);

@@ -226,6 +226,160 @@ int build_rechalving(int P, int me, uint64_t count, uint64_t ts, unsigned dst_mi
     return SOSX_OK;
 }
 
+// Team prefix scan (SOS scan_ring semantics, src/collectives.c:1111-1209): PE i's result
+// is ((s_0 OP s_1) OP ...) OP s_i (inscan) or the same over s_0..s_{i-1} with PE 0
+// zeroed (exscan).  Ring chunk c of every source is gathered at PE c, one PREFIX pass
+// yields chunk c of all P results, a direct all-to-all hands them out.
+int build_scan(bool exclusive, int P, int me, uint64_t count, uint64_t ts, unsigned src_mis,
+               unsigned dst_mis, Plan *plan)
+{
+    if (P > PLAN_MAX_PE) return SOSX_ERR_ARG;
+    uint64_t n_me, first_me;
+    ring_chunk(count, P, me, &n_me, &first_me);
+    const uint64_t my_bytes = n_me * ts;
+    const uint64_t mis = (dst_mis + first_me * ts) & 15;
+    const uint64_t stride = round_up(my_bytes + 16, 256);
+    (void)src_mis;
+    // SCR: P-1 slots for the peers' copies of my chunk, then P-1 slots for my chunk of
+    // the peers' results
+    auto idx = [&](int peer) { return (uint64_t)((peer - me - 1 + P) % P); };
+    auto slot_in = [&](int peer) { return idx(peer) * stride + mis; };
+    auto slot_out = [&](int peer) { return ((uint64_t)(P - 1) + idx(peer)) * stride + mis; };
+    plan->scratch_bytes = 2 * (uint64_t)(P - 1) * stride;
+    plan->scr_sent = true;
+
+    Round g;  // gather chunk `me` of every source
+    for (int k = 1; k < P; ++k) {
+        const int peer = (me + k) % P;
+        uint64_t n_p, first_p;
+        ring_chunk(count, P, peer, &n_p, &first_p);
+        if (n_p) g.xfers.push_back(xf(1, peer, SRC, first_p * ts, n_p * ts));
+        if (n_me) g.xfers.push_back(xf(0, peer, SCR, slot_in(peer), my_bytes));
+    }
+    if (n_me) {
+        auto in_of = [&](int pe, int *b, uint64_t *o) {
+            *b = pe == me ? SRC : SCR;
+            *o = pe == me ? first_me * ts : slot_in(pe);
+        };
+        auto out_of = [&](int pe, int *b, uint64_t *o) {
+            *b = pe == me ? DST : SCR;
+            *o = pe == me ? first_me * ts : slot_out(pe);
+        };
+        Local l;
+        memset(&l, 0, sizeof(l));
+        l.kind = PREFIX;
+        l.count = n_me;
+        l.own = -1;
+        // inscan: outs[k] (PE k) = prefix(ins[0..k]); exscan: outs[k] (PE k+1) = prefix(ins[0..k])
+        const int nin = exclusive ? P - 1 : P;
+        l.nin = l.nout = nin;
+        for (int k = 0; k < nin; ++k) {
+            in_of(k, &l.in_buf[k], &l.in_off[k]);
+            out_of(exclusive ? k + 1 : k, &l.outs_buf[k], &l.outs_off[k]);
+            if (k == me) l.own = k;
+        }
+        l.out_buf = l.outs_buf[0];
+        l.out_off = l.outs_off[0];
+        g.ops.push_back(l);
+        if (exclusive) {
+            // PE 0's result is zero (src/collectives.c:1145-1155); after the PREFIX pass,
+            // which may still read my source chunk where it aliases the target
+            Local z;
+            memset(&z, 0, sizeof(z));
+            z.kind = ZERO;
+            out_of(0, &z.out_buf, &z.out_off);
+            z.count = my_bytes;
+            g.ops.push_back(z);
+        }
+    }
+    plan->rounds.push_back(g);
+
+    Round a;  // all-to-all of the result chunks
+    for (int k = 1; k < P; ++k) {
+        const int peer = (me + k) % P;
+        uint64_t n_p, first_p;
+        ring_chunk(count, P, peer, &n_p, &first_p);
+        if (n_me) a.xfers.push_back(xf(1, peer, SCR, slot_out(peer), my_bytes));
+        if (n_p) a.xfers.push_back(xf(0, peer, DST, first_p * ts, n_p * ts));
+    }
+    plan->rounds.push_back(a);
+    return SOSX_OK;
+}
+
+// Broadcast from team index `root` (src/collectives.c:429-485).  Payloads of at least
+// kBcastSplitBytes over P > 2 PEs: the root scatters P-1 chunks (one per non-root, each
+// over its own link), the non-roots exchange them directly -- every link carries ~1/(P-1)
+// of the payload per round instead of the root's link(s) carrying P-1 copies.
+constexpr uint64_t kBcastSplitBytes = 64 * 1024;
+
+int build_bcast(int root, bool copy_root, int P, int me, uint64_t count, uint64_t ts, Plan *plan)
+{
+    if (root < 0 || root >= P) return SOSX_ERR_ARG;
+    const uint64_t bytes = count * ts;
+    plan->reads_src = me == root;
+    plan->writes_dst = me != root || copy_root;
+    Round r;
+    if (me == root && copy_root) {
+        Local l;
+        memset(&l, 0, sizeof(l));
+        l.kind = COPY;
+        l.out_buf = DST;
+        l.nin = 1;
+        l.in_buf[0] = SRC;
+        l.count = bytes;
+        r.ops.push_back(l);
+    }
+    if (P == 1) {
+        plan->rounds.push_back(r);
+        return SOSX_OK;
+    }
+    if (P == 2 || bytes < kBcastSplitBytes) {
+        for (int k = 1; k < P; ++k) {
+            const int peer = (root + k) % P;
+            if (me == root) r.xfers.push_back(xf(1, peer, SRC, 0, bytes));
+            else if (me == peer) r.xfers.push_back(xf(0, root, DST, 0, bytes));
+        }
+        plan->rounds.push_back(r);
+        return SOSX_OK;
+    }
+    // chunk j (j = 0..P-2) belongs to the j-th non-root in ring order after the root;
+    // chunks are cut in 64-B units when the element size divides 64
+    const uint64_t unit = (64 % ts == 0) ? 64 / ts : 1;
+    const uint64_t units = (count + unit - 1) / unit;
+    auto chunk = [&](int j, uint64_t *off, uint64_t *len) {
+        uint64_t n, first;
+        ring_chunk(units, P - 1, j, &n, &first);
+        uint64_t lo = first * unit, hi = (first + n) * unit;
+        if (lo > count) lo = count;
+        if (hi > count) hi = count;
+        *off = lo * ts;
+        *len = (hi - lo) * ts;
+    };
+    auto owner = [&](int j) { return (root + 1 + j) % P; };
+    const int mine = me == root ? -1 : (me - root - 1 + P) % P;
+    for (int j = 0; j < P - 1; ++j) {  // scatter
+        uint64_t off, len;
+        chunk(j, &off, &len);
+        if (!len) continue;
+        if (me == root) r.xfers.push_back(xf(1, owner(j), SRC, off, len));
+        else if (j == mine) r.xfers.push_back(xf(0, root, DST, off, len));
+    }
+    plan->rounds.push_back(r);
+    if (me == root) return SOSX_OK;
+    Round ag;  // allgather among the non-roots
+    uint64_t moff, mlen;
+    chunk(mine, &moff, &mlen);
+    for (int k = 1; k < P - 1; ++k) {
+        const int j = (mine + k) % (P - 1);
+        uint64_t off, len;
+        chunk(j, &off, &len);
+        if (mlen) ag.xfers.push_back(xf(1, owner(j), DST, moff, mlen));
+        if (len) ag.xfers.push_back(xf(0, owner(j), DST, off, len));
+    }
+    plan->rounds.push_back(ag);
+    return SOSX_OK;
+}
+
 }  // namespace
 
 void ring_chunk(uint64_t count, int P, int c, uint64_t *n, uint64_t *first)
@@ -250,7 +404,27 @@ int build(int alg, int P, int me, uint64_t count, uint64_t ts, unsigned src_mis,
     out->alg = alg;
     out->rounds.clear();
     out->scratch_bytes = 0;
+    out->reads_src = out->writes_dst = true;
+    out->scr_sent = false;
     if (count == 0) return SOSX_OK;
+    if (is_bcast(alg))
+        return build_bcast((alg - PLAN_BCAST) >> 1, (alg - PLAN_BCAST) & 1, P, me, count, ts, out);
+    if (is_scan(alg) && P == 1) {
+        // PE_size 1: inscan copies, exscan zeroes (src/collectives.c:1145-1166)
+        Round r;
+        Local l;
+        memset(&l, 0, sizeof(l));
+        l.kind = alg == PLAN_EXSCAN ? ZERO : COPY;
+        l.out_buf = DST;
+        l.nin = alg == PLAN_EXSCAN ? 0 : 1;
+        l.in_buf[0] = SRC;
+        l.count = count * ts;
+        r.ops.push_back(l);
+        out->rounds.push_back(r);
+        out->reads_src = alg != PLAN_EXSCAN;
+        return SOSX_OK;
+    }
+    if (is_scan(alg)) return build_scan(alg == PLAN_EXSCAN, P, me, count, ts, src_mis, dst_mis, out);
     if (P == 1) {
         // PE_size == 1: the reference copies source to target (src/collectives.c:664-668)
         Round r;
@@ -284,7 +458,8 @@ int build(int alg, int P, int me, uint64_t count, uint64_t ts, unsigned src_mis,
 // C ABI: plan introspection (CPU tests simulate every PE's plan against the oracle)
 // Encoding (int64 words): [alg, nrounds, scratch_bytes,
 //   per round: nx, nops, nx * (send, peer, buf, off, bytes),
-//              nops * (kind, order, out_buf, out_off, nin, count, nin * (buf, off))]
+//              nops * (kind, order, out_buf, out_off, nin, count, nin * (buf, off),
+//                      nout, nout * (buf, off))]
 // Returns the number of words (the buffer is filled only if cap >= that), or < 0.
 // --------------------------------------------------------------------------------
 extern "C" long long sosx_plan_encode(int alg, int P, int me, unsigned long long count,
@@ -318,6 +493,11 @@ extern "C" long long sosx_plan_encode(int alg, int P, int me, unsigned long long
             for (int k = 0; k < l.nin; ++k) {
                 w.push_back(l.in_buf[k]);
                 w.push_back((long long)l.in_off[k]);
+            }
+            w.push_back(l.kind == sosplan::PREFIX ? l.nout : 0);
+            for (int k = 0; l.kind == sosplan::PREFIX && k < l.nout; ++k) {
+                w.push_back(l.outs_buf[k]);
+                w.push_back((long long)l.outs_off[k]);
             }
         }
     }

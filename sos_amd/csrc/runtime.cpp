@@ -11,6 +11,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <string>
 
 #include "bootstrap.h"
@@ -25,6 +26,7 @@ extern "C" char _end[] __attribute__((weak));
 extern "C" {
 shmem_team_t SHMEM_TEAM_WORLD = nullptr;
 shmem_team_t SHMEM_TEAM_SHARED = nullptr;
+shmem_team_t SHMEMX_TEAM_NODE = nullptr;
 }
 
 namespace sosrt {
@@ -134,6 +136,9 @@ static void read_env(State &s)
 {
     s.reduce_alg = parse_reduce_alg(getenv2("REDUCE_ALGORITHM"), SOSX_ALG_AUTO);
     s.coll_size_crossover = atol_scaled(getenv2("COLL_SIZE_CROSSOVER"), 16384);
+    // SHMEM_TEAMS_MAX (src/shmem_env_defs.h:75, default 10; src/shmem_team.c:171-178)
+    const char *tm = getenv2("TEAMS_MAX");
+    s.teams_max = tm && *tm ? atol(tm) : 10;
     s.symmetric_size = atol_scaled(getenv2("SYMMETRIC_SIZE"), 512u << 20);
     const char *d = getenv2("DEBUG");
     s.debug = d && *d && strcmp(d, "0") && strcasecmp(d, "false");
@@ -391,9 +396,20 @@ static void init_common(int pe, int npes, const ncclUniqueId *uid)
     s.world.my_idx = pe;
     s.world.valid = true;
     s.world.predefined = true;
-    s.shared = s.world;  // one node: every PE shares it
+    s.world.psync_idx = 0;
+    s.shared = s.world;  // one node: every PE shares it (src/shmem_team.c:88-140)
+    s.shared.psync_idx = 1;
+    s.node = s.world;    // SHMEMX_TEAM_NODE (:101-164)
+    s.node.psync_idx = 2;
     SHMEM_TEAM_WORLD = &s.world;
     SHMEM_TEAM_SHARED = &s.shared;
+    SHMEMX_TEAM_NODE = &s.node;
+    // team slots (src/shmem_team.c:171-226): 64 at most, 3 at least, 0..2 predefined
+    if (s.teams_max > 64) raise_error("Requested %ld teams, but only 64 are supported", s.teams_max);
+    if (s.teams_max < 3) s.teams_max = 3;
+    s.team_avail = 0;
+    for (long i = 3; i < s.teams_max; ++i) s.team_avail |= 1ull << i;
+    s.team_pool.assign((size_t)s.teams_max, nullptr);
     s.initialized = true;
     s.finalized = false;
     if (s.want_p2p || s.ext_base) ensure_device_heap();
@@ -511,6 +527,13 @@ void shmem_finalize(void)
     State &s = st();
     if (!s.initialized) return;
     team_barrier(s.world);
+    // destroy the teams the program left (src/shmem_team.c:238-247)
+    for (size_t i = 3; i < s.team_pool.size(); ++i)
+        if (s.team_pool[i]) {
+            s.team_pool[i]->valid = false;
+            delete s.team_pool[i];
+            s.team_pool[i] = nullptr;
+        }
     if (s.comm) ncclCommDestroy(s.comm);
     s.comm = nullptr;
     if (s.scratch) (void)hipFree(s.scratch);
@@ -797,51 +820,131 @@ int shmem_team_n_pes(shmem_team_t team)
 
 int shmem_team_get_config(shmem_team_t team, long config_mask, shmem_team_config_t *config)
 {
-    team_checked(team, "shmem_team_get_config");
-    if (config && (config_mask & SHMEM_TEAM_NUM_CONTEXTS)) config->num_contexts = 0;
+    // src/teams_c.c4:76-100
+    check_initialized("shmem_team_get_config");
+    if (team == SHMEM_TEAM_INVALID) return -1;
+    Team *t = team_checked(team, "shmem_team_get_config");
+    if (config_mask != 0) {
+        if (config_mask != SHMEM_TEAM_NUM_CONTEXTS) {
+            warn("Invalid team config mask (%ld)", config_mask);
+            return -1;
+        }
+        if (!config) {
+            warn("NULL config pointer passed to shmem_team_get_config");
+            return -1;
+        }
+        config->num_contexts = t->num_contexts;
+    } else if (config) {
+        warn("shmem_team_get_config encountered an unexpected non-NULL config structure "
+             "passed with a config_mask of 0.");
+    }
     return 0;
 }
 
 int shmem_team_translate_pe(shmem_team_t src_team, int src_pe, shmem_team_t dest_team)
 {
+    // src/shmem_team.c:262-283
+    check_initialized("shmem_team_translate_pe");
     if (src_team == SHMEM_TEAM_INVALID || dest_team == SHMEM_TEAM_INVALID) return -1;
     Team *s = team_checked(src_team, "shmem_team_translate_pe");
     Team *d = team_checked(dest_team, "shmem_team_translate_pe");
     if (src_pe < 0 || src_pe >= s->size) return -1;
-    const int g = s->world_rank(src_pe);
-    if (g < d->start || (g - d->start) % d->stride) return -1;
-    const int idx = (g - d->start) / d->stride;
+    const int off = s->world_rank(src_pe) - d->start;  // shmem_internal_pe_in_active_set
+    if ((d->stride > 0 ? off < 0 : off > 0) || off % d->stride) return -1;
+    const int idx = off / d->stride;
     return idx < d->size ? idx : -1;
+}
+
+// Team creation agreement over the parent (src/shmem_team.c:354-432): the members AND
+// their free-slot masks and take the lowest common slot; every parent PE then returns
+// the MAX of the members' status, so all agree.  Node shared memory carries the words.
+static int team_agree_slot(const Team &parent, const Team &child, bool member, int *slot)
+{
+    State &s = st();
+    const bool shm = parent.size > 1 && s.shm.extra;
+    const int me_world = s.my_pe;
+    *slot = -1;
+    if (shm) {
+        team_word_put(0, me_world, member ? s.team_avail : 0);
+        team_barrier(parent);
+    }
+    int status = 0;
+    if (member) {
+        uint64_t all = s.team_avail;
+        for (int i = 0; shm && i < child.size; ++i) all &= team_word_get(0, child.world_rank(i));
+        const int idx = all ? __builtin_ctzll(all) : -1;
+        if (idx < 0 || idx >= s.teams_max) {
+            warn("No more teams available (max = %ld), try increasing SHMEM_TEAMS_MAX", s.teams_max);
+            status = 1;
+        } else {
+            *slot = idx;
+        }
+    }
+    if (!shm) return status;
+    team_word_put(1, me_world, (uint64_t)status);
+    team_barrier(parent);
+    int agreed = 0;
+    for (int i = 0; i < parent.size; ++i)
+        agreed = std::max(agreed, (int)team_word_get(1, parent.world_rank(i)));
+    return agreed;
 }
 
 int shmem_team_split_strided(shmem_team_t parent_team, int PE_start, int PE_stride, int PE_size,
                              const shmem_team_config_t *config, long config_mask,
                              shmem_team_t *new_team)
 {
-    (void)config;
-    (void)config_mask;
-    Team *parent = team_checked(parent_team, "shmem_team_split_strided");
+    check_initialized("shmem_team_split_strided");
     if (new_team) *new_team = SHMEM_TEAM_INVALID;
-    // argument rules of src/shmem_team.c:300-321
-    if (PE_start < 0 || PE_start >= parent->size || PE_size <= 0 || PE_size > parent->size ||
-        PE_stride < 1 || PE_start + (PE_size - 1) * PE_stride >= parent->size) {
+    if (parent_team == SHMEM_TEAM_INVALID) return 1;  // src/shmem_team.c:296-298
+    Team *parent = team_checked(parent_team, "shmem_team_split_strided");
+    State &s = st();
+    // argument rules of src/shmem_team.c:300-321: a stride of 0 (or a 1-PE team) is 1,
+    // and the child's first/last PE must be valid world PEs; no collective on error
+    PE_stride = (PE_stride == 0 || PE_size == 1) ? 1 : PE_stride;
+    if (PE_start < 0 || PE_start >= parent->size || PE_size <= 0 || PE_size > parent->size) {
         warn("Invalid <start, stride, size>: child <%d, %d, %d>, parent <%d, %d, %d>", PE_start,
              PE_stride, PE_size, parent->start, parent->stride, parent->size);
-        team_barrier(*parent);
+        return -1;
+    }
+    const int gstart = parent->world_rank(PE_start);
+    const int gstride = parent->stride * PE_stride;
+    const int gend = gstart + gstride * (PE_size - 1);
+    if (gstart < 0 || gstart >= s.n_pes) {
+        warn("Starting global PE (%d) is invalid", gstart);
+        return -1;
+    }
+    if (gend < 0 || gend >= s.n_pes) {
+        warn("Ending global PE (%d) is invalid", gend);
+        return -1;
+    }
+    if (config_mask != 0 && config_mask != SHMEM_TEAM_NUM_CONTEXTS) {
+        warn("Invalid team_split_strided config_mask (%ld)", config_mask);
         return -1;
     }
     Team child;
-    child.start = parent->world_rank(PE_start);
-    child.stride = parent->stride * PE_stride;
+    child.start = gstart;
+    child.stride = PE_size == 1 ? 1 : gstride;
     child.size = PE_size;
     child.valid = true;
-    const int my = parent->my_idx;
-    if (my >= PE_start && (my - PE_start) % PE_stride == 0 && (my - PE_start) / PE_stride < PE_size) {
-        child.my_idx = (my - PE_start) / PE_stride;
-        if (new_team) *new_team = new Team(child);
+    child.config_mask = config_mask;
+    child.num_contexts = config_mask && config ? config->num_contexts : 0;
+    const int d = s.my_pe - gstart;
+    const bool member = gstride > 0 ? (d >= 0 && d % gstride == 0 && d / gstride < PE_size)
+                                    : (d <= 0 && (-d) % (-gstride) == 0 && (-d) / (-gstride) < PE_size);
+    if (member) child.my_idx = d / gstride;
+    int slot = -1;
+    const int rc = team_agree_slot(*parent, child, member, &slot);
+    if (member && slot >= 0) {
+        child.psync_idx = slot;
+        if (rc == 0) {
+            s.team_avail &= ~(1ull << slot);
+            Team *t = new Team(child);
+            s.team_pool[(size_t)slot] = t;
+            if (new_team) *new_team = t;
+        }
     }
-    team_barrier(*parent);
-    return 0;
+    team_barrier(*parent);  // src/shmem_team.c:410-414
+    return rc;
 }
 
 int shmem_team_split_2d(shmem_team_t parent_team, int xrange, const shmem_team_config_t *xaxis_config,
@@ -849,32 +952,56 @@ int shmem_team_split_2d(shmem_team_t parent_team, int xrange, const shmem_team_c
                         const shmem_team_config_t *yaxis_config, long yaxis_mask,
                         shmem_team_t *yaxis_team)
 {
-    // src/shmem_team.c:436-505: x teams are consecutive runs of xrange PEs, y teams
-    // stride xrange through the parent.
+    // src/shmem_team.c:436-505: every x team (consecutive runs of xrange) and then every
+    // y team (stride xrange) is created by a split over the whole parent, in order
+    check_initialized("shmem_team_split_2d");
+    if (xaxis_team) *xaxis_team = SHMEM_TEAM_INVALID;
+    if (yaxis_team) *yaxis_team = SHMEM_TEAM_INVALID;
+    if (parent_team == SHMEM_TEAM_INVALID) return 1;
     Team *parent = team_checked(parent_team, "shmem_team_split_2d");
-    if (xrange <= 0) {
+    if (xrange <= 0) {  // SOS divides by xrange (:455)
         warn("Invalid xrange (%d)", xrange);
         return -1;
     }
     if (xrange > parent->size) xrange = parent->size;
-    const int my = parent->my_idx;
-    const int xstart = my / xrange * xrange;
-    const int xsize = (parent->size - xstart) < xrange ? parent->size - xstart : xrange;
-    int rc = shmem_team_split_strided(parent_team, xstart, 1, xsize, xaxis_config, xaxis_mask,
-                                      xaxis_team);
-    // every PE must take part in every split of the parent: run all x splits in order
-    (void)rc;
-    const int ystart = my % xrange;
-    const int ysize = (parent->size - ystart + xrange - 1) / xrange;
-    rc = shmem_team_split_strided(parent_team, ystart, xrange, ysize, yaxis_config, yaxis_mask,
-                                  yaxis_team);
-    return rc;
+    const int psize = parent->size;
+    const int num_xteams = (psize + xrange - 1) / xrange;
+    int start = 0;
+    for (int i = 0; i < num_xteams; ++i) {
+        const int xsize = (i == num_xteams - 1 && psize % xrange) ? psize % xrange : xrange;
+        shmem_team_t t = SHMEM_TEAM_INVALID;
+        if (shmem_team_split_strided(parent_team, start, 1, xsize, xaxis_config, xaxis_mask, &t))
+            raise_error("Creation of x-axis team %d of %d failed", i + 1, num_xteams);
+        start += xrange;
+        if (t != SHMEM_TEAM_INVALID && xaxis_team) *xaxis_team = t;
+    }
+    start = 0;
+    for (int i = 0; i < xrange; ++i) {
+        const int rem = psize % xrange, yrange = psize / xrange;
+        const int ysize = (rem && i < rem) ? yrange + 1 : yrange;
+        shmem_team_t t = SHMEM_TEAM_INVALID;
+        if (shmem_team_split_strided(parent_team, start, xrange, ysize, yaxis_config, yaxis_mask, &t))
+            raise_error("Creation of y-axis team %d of %d failed", i + 1, xrange);
+        start += 1;
+        if (t != SHMEM_TEAM_INVALID && yaxis_team) *yaxis_team = t;
+    }
+    team_barrier(*parent);
+    return 0;
 }
 
 void shmem_team_destroy(shmem_team_t team)
 {
+    // src/teams_c.c4:138-148, src/shmem_team.c:508-535
+    check_initialized("shmem_team_destroy");
+    State &s = st();
+    if (team == &s.world || team == &s.shared)
+        raise_error("Cannot destroy a pre-defined team");
     Team *t = team_from_handle(team);
     if (!t || t->predefined) return;
+    if (t->psync_idx >= 3 && t->psync_idx < (int)s.team_pool.size() && s.team_pool[(size_t)t->psync_idx] == t) {
+        s.team_pool[(size_t)t->psync_idx] = nullptr;
+        s.team_avail |= 1ull << t->psync_idx;
+    }
     t->valid = false;
     delete t;
 }

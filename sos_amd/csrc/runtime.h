@@ -39,6 +39,9 @@ struct Team {
     int start = 0, stride = 1, size = 1;
     int my_idx = -1;          // index of this PE in the team, -1 if not a member
     int psync_avail[2] = {1, 1};  // SOS N_PSYNCS_PER_TEAM (src/shmem_team.h:18)
+    int psync_idx = -1;           // team slot (src/shmem_team.c:21-24, :381-405)
+    long config_mask = 0;         // shmem_team_config_t given at creation
+    int num_contexts = 0;
     bool valid = false;
     bool predefined = false;
     int world_rank(int idx) const { return start + idx * stride; }
@@ -102,8 +105,12 @@ struct State {
     bool debug = false;
     bool error_checking = true;
     bool heap_on_device = false;
-    // teams
-    Team world, shared;
+    // teams (src/shmem_team.c): predefined WORLD / SHARED / SHMEMX_TEAM_NODE occupy slots
+    // 0..2 of SHMEM_TEAMS_MAX; team_avail has a bit per free slot
+    Team world, shared, node;
+    long teams_max = 10;
+    uint64_t team_avail = 0;
+    std::vector<Team *> team_pool;
     std::mutex mu;
 };
 
@@ -140,6 +147,8 @@ void ensure_device_heap();
 
 // Per-pair transport counters living in the shared-memory segment (p2p.cpp).
 size_t p2p_shared_bytes();
+void team_word_put(int which, int world_pe, uint64_t v);   // node shm (p2p.cpp)
+uint64_t team_word_get(int which, int world_pe);
 
 }  // namespace sosrt
 
@@ -151,6 +160,8 @@ struct P2PBufs {
     char *dst;
     char *scr;
     size_t src_off, dst_off;  // heap offsets of src/dst (published to the peers)
+    size_t scr_off;           // heap offset of scr when the plan sends out of it
+    unsigned smis, dmis;      // src/dst address mod 16 the plan was built with
 };
 int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, uint64_t ts,
              const P2PBufs &b, int op, int dt, hipStream_t stream);

@@ -27,6 +27,11 @@ _RUNTIME = {
     "shmem_team_split_strided": (_c.c_int, [_c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p,
                                             _c.c_long, _c.POINTER(_c.c_void_p)]),
     "shmem_team_destroy": (None, [_c.c_void_p]),
+    "shmem_team_split_2d": (_c.c_int, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_long,
+                                       _c.POINTER(_c.c_void_p), _c.c_void_p, _c.c_long,
+                                       _c.POINTER(_c.c_void_p)]),
+    "shmem_team_translate_pe": (_c.c_int, [_c.c_void_p, _c.c_int, _c.c_void_p]),
+    "shmem_team_get_config": (_c.c_int, [_c.c_void_p, _c.c_long, _c.c_void_p]),
     "shmem_team_sync": (_c.c_int, [_c.c_void_p]),
     "shmemx_get_unique_id": (_c.c_int, [_c.c_void_p, _c.c_size_t]),
     "shmemx_init_attr": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _c.c_size_t]),
@@ -45,12 +50,19 @@ _RUNTIME = {
                                          _c.c_ulonglong, _c.c_uint, _c.c_uint,
                                          _c.POINTER(_c.c_longlong), _c.c_ulonglong]),
     "sosx_resolve_alg": (_c.c_int, [_c.c_int, _c.c_ulonglong, _c.c_ulonglong]),
+    "shmem_broadcastmem": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_int]),
+    "shmem_broadcast32": (None, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_int, _c.c_int, _c.c_int,
+                                 _c.c_int, _c.c_void_p]),
+    "shmem_broadcast64": (None, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_int, _c.c_int, _c.c_int,
+                                 _c.c_int, _c.c_void_p]),
     "sosx_prof_enable": (None, [_c.c_int]),
     "sosx_prof_get": (None, [_c.POINTER(_c.c_double), _c.POINTER(_c.c_double),
                              _c.POINTER(_c.c_long), _c.POINTER(_c.c_long), _c.POINTER(_c.c_long)]),
 }
 
 _REDUCE_RE = re.compile(r"^shmem_(\w+?)_(and|or|xor|min|max|sum|prod)_(reduce|to_all)$")
+_SCAN_RE = re.compile(r"^shmemx_(\w+?)_sum_(inscan|exscan)$")
+_BCAST_RE = re.compile(r"^shmem_(\w+?)_broadcast$")
 _declared = False
 
 
@@ -74,6 +86,10 @@ def team_shared():
     return ctypes.c_void_p.in_dll(lib(), "SHMEM_TEAM_SHARED").value
 
 
+def team_node():
+    return ctypes.c_void_p.in_dll(lib(), "SHMEMX_TEAM_NODE").value
+
+
 def __getattr__(name):
     """shmem_<T>_<op>_reduce / _to_all, shmem_init, ... resolved from the library."""
     L = lib()
@@ -87,6 +103,16 @@ def __getattr__(name):
             fn.restype = None
             fn.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                            _c.c_void_p, _c.c_void_p]
+        return fn
+    if _SCAN_RE.match(name):
+        fn = getattr(L, name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t]
+        return fn
+    if _BCAST_RE.match(name):
+        fn = getattr(L, name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_int]
         return fn
     if name in _RUNTIME:
         return getattr(L, name)
@@ -141,7 +167,14 @@ def plan(alg, P, me, count, ts, src_mis=0, dst_mis=0):
             for _ in range(nin):
                 ins.append((w[pos], w[pos + 1]))
                 pos += 2
-            ops.append({"kind": kind, "order": order, "out": (ob, ooff), "ins": ins, "count": cnt})
+            nout = w[pos]
+            pos += 1
+            outs = []
+            for _ in range(nout):
+                outs.append((w[pos], w[pos + 1]))
+                pos += 2
+            ops.append({"kind": kind, "order": order, "out": (ob, ooff), "ins": ins, "count": cnt,
+                        "outs": outs})
         rounds.append({"xfers": xfers, "ops": ops})
     return {"alg": w[0], "scratch_bytes": w[2], "rounds": rounds}
 

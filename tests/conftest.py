@@ -11,6 +11,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+if os.environ.get("SOSX_CRASHTRACE") == "1":  # diagnostics: native backtrace on abort
+    import ctypes
+    ctypes.CDLL(os.path.join(ROOT, "tools", "diag", "libcrashtrace.so"))
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X) and libsos_amd.so")

@@ -11,7 +11,7 @@ from oracle import oracle as O
 from sos_amd import shmem as S
 
 SRC, DST, SCR = 0, 1, 2
-FOLD, COPY = 0, 1
+FOLD, COPY, PREFIX, ZERO = 0, 1, 2, 3
 LINEAR, TREE = 0, 1
 
 
@@ -37,17 +37,25 @@ def fold_values(op, dt, ins, order):
     return w[0]
 
 
-def simulate(alg, op, dt, srcs, in_place=False):
-    """Run all PEs' plans; returns the list of per-PE target arrays."""
+def simulate(alg, op, dt, srcs, in_place=False, dsts=None, mis=(0, 0)):
+    """Run all PEs' plans; returns the list of per-PE target arrays.
+
+    `dsts` gives the targets' initial contents (default zeros); `mis` the (src, dst)
+    addresses mod 16 the plans are built for."""
     P = len(srcs)
     n = srcs[0].size
     ts = srcs[0].itemsize
     np_t = srcs[0].dtype
-    plans = [S.plan(alg, P, p, n, ts) for p in range(P)]
+    plans = [S.plan(alg, P, p, n, ts, mis[0], mis[1]) for p in range(P)]
     bufs = []
     for p in range(P):
         src = bytearray(srcs[p].tobytes())
-        dst = src if in_place else bytearray(n * ts)
+        if in_place:
+            dst = src
+        elif dsts is not None:
+            dst = bytearray(dsts[p].tobytes())
+        else:
+            dst = bytearray(n * ts)
         bufs.append({SRC: src, DST: dst, SCR: bytearray(max(plans[p]["scratch_bytes"], 1))})
     fifo = {}
     k = [0] * P
@@ -96,9 +104,22 @@ def simulate(alg, op, dt, srcs, in_place=False):
                         ib, ioff = l["ins"][0]
                         bufs[p][ob][ooff:ooff + l["count"]] = bytes(bufs[p][ib][ioff:ioff + l["count"]])
                         continue
+                    if l["kind"] == ZERO:
+                        bufs[p][ob][ooff:ooff + l["count"]] = bytes(l["count"])
+                        continue
                     cnt = l["count"]
                     ins = [np.frombuffer(bytes(bufs[p][b][o:o + cnt * ts]), dtype=np_t)
                            for b, o in l["ins"]]
+                    if l["kind"] == PREFIX:
+                        # all inputs are read before any output is written (kernel contract)
+                        acc = ins[0].copy()
+                        outs = [acc.copy()]
+                        for x in ins[1:]:
+                            O.reduce_local(op, dt, x, acc)
+                            outs.append(acc.copy())
+                        for (b, o), v in zip(l["outs"], outs):
+                            bufs[p][b][o:o + cnt * ts] = v.tobytes()
+                        continue
                     res = fold_values(op, dt, ins, l["order"])
                     bufs[p][ob][ooff:ooff + cnt * ts] = res.tobytes()
                 k[p] += 1

@@ -15,7 +15,7 @@ REF_PI = "/root/reference/examples/pi_reduce.c"
 
 def declared_functions():
     names = set()
-    for h in ("shmem.h", "shmemx.h", "sosx.h", "shmem_reductions.h"):
+    for h in ("shmem.h", "shmemx.h", "sosx.h", "shmem_reductions.h", "shmemx_scans.h"):
         text = open(os.path.join(INC, h)).read()
         text = text.split("#if defined(__cplusplus)\nstatic inline")[0]  # skip inline overloads
         for m in re.finditer(r"^\s*(?:SHMEM_FUNCTION_ATTRIBUTES\s+)?(?:const\s+)?[\w ]+?\**\s*\b(\w+)\(",
@@ -36,16 +36,19 @@ def test_library_loads_and_exports_everything():
     from sos_amd import _lib
     _lib.lib()
     declared = declared_functions()
-    assert len(declared) > 400  # 198 shmem_* + 198 pshmem_* reductions + runtime + sosx
+    assert len(declared) > 550  # 274 typed shmem_* + their pshmem_* + runtime + sosx
     missing = sorted(declared - exported_symbols())
     assert not missing, missing
 
 
-def test_198_reduction_symbols():
+def test_typed_collective_symbols():
+    # 198 reductions (44 to_all + 154 reduce), 24 typed broadcasts, 52 sum scans
     sys.path.insert(0, os.path.join(ROOT, "sos_amd", "csrc"))
     import gen_bindings
     names = gen_bindings.symbols()
-    assert len(names) == 198 and len(set(names)) == 198
+    assert len(names) == 274 and len(set(names)) == 274
+    assert sum(n.endswith("_broadcast") for n in names) == 24
+    assert sum(n.endswith(("_inscan", "_exscan")) for n in names) == 52
     exp = exported_symbols()
     assert all(n in exp and "p" + n in exp for n in names)
     # SOS quirks carried over: uint8..64 reduce with the SIGNED internal type
@@ -100,6 +103,21 @@ def test_cxx_overloads_compile(tmp_path):
                    'shmem_sum_reduce(SHMEM_TEAM_WORLD, &a, &b, 1); shmem_max_reduce(SHMEM_TEAM_WORLD, d, e, 4);\n'
                    'shmem_xor_reduce(SHMEM_TEAM_WORLD, u, v, 3); shmem_finalize(); return 0; }\n')
     _compile(str(src), "cxx", tmp_path)
+
+
+def test_bcast_scan_generics_compile(tmp_path):
+    body = ('static long long a[4], b[4]; static double d[4], e[4]; static int i4[4], j4[4];\n'
+            'static long ps[SHMEM_BCAST_SYNC_SIZE];\n'
+            'shmem_broadcast(SHMEM_TEAM_WORLD, a, b, 4, 0); shmem_broadcast(SHMEM_TEAM_WORLD, d, e, 4, 0);\n'
+            'shmem_broadcastmem(SHMEM_TEAM_WORLD, i4, j4, sizeof i4, 0);\n'
+            'shmem_broadcast64(a, b, 4, 0, 0, 0, shmem_n_pes(), ps);\n'
+            'shmem_broadcast32(i4, j4, 4, 0, 0, 0, shmem_n_pes(), ps);\n'
+            'shmemx_sum_inscan(SHMEM_TEAM_WORLD, d, e, 4); shmemx_sum_exscan(SHMEM_TEAM_WORLD, i4, j4, 4);\n')
+    for lang, ext, hdr in (("c", "c", "#include <shmem.h>\n#include <shmemx.h>\n"),
+                           ("cxx", "cpp", "#include <shmem.h>\n#include <shmemx.h>\n")):
+        src = tmp_path / f"t.{ext}"
+        src.write_text(hdr + "int main(void){ shmem_init();\n" + body + "shmem_finalize(); return 0; }\n")
+        _compile(str(src), lang, tmp_path)
 
 
 def test_plan_abi_rejects_bad_args():

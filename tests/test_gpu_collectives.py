@@ -1,0 +1,165 @@
+"""GPU: the team scans and broadcast, and the runtime-P fold (teams above 8 PEs).
+
+Every result is compared bit for bit with the CPU oracle (oracle/sos_oracle.c):
+  sosx_prefix                 == in-order prefix of oracle reduce_local
+  loopback inscan / exscan    == oracle_scan   (SOS scan_ring, src/collectives.c:1111-1209)
+  loopback broadcast          == oracle_bcast  (src/collectives.c:429-485)
+  sosx_fold with 9..64 inputs == the plan simulator's LINEAR / TREE fold
+  loopback ring over 12 PEs   == oracle_ring   (src/collectives.c:647-764)
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from sos_amd import _lib, shmem as S
+
+import plansim
+
+pytestmark = pytest.mark.gpu
+
+
+def to_dev(torch, a, pad=0):
+    """Device copy of array a (bytes), optionally `pad` bytes into a larger buffer."""
+    raw = np.frombuffer(a.tobytes(), np.uint8)
+    t = torch.zeros(raw.size + pad + 16, dtype=torch.uint8, device="cuda")
+    t[pad:pad + raw.size].copy_(torch.from_numpy(raw.copy()))
+    return t
+
+
+def from_dev(t, like, pad=0):
+    raw = t[pad:pad + like.nbytes].cpu().numpy()
+    return np.frombuffer(raw.tobytes(), like.dtype).copy()
+
+
+def bits(a):
+    return np.frombuffer(a.tobytes(), np.uint8)
+
+
+def src_of(dt, seed, pe, n):
+    if dt == 25:
+        return np.random.default_rng(seed * 131 + pe).standard_normal(n).astype(np.longdouble)
+    return O.fill(dt, 0, seed, pe, n)
+
+
+def cpu_prefix(op, dt, ins):
+    acc = ins[0].copy()
+    outs = [acc.copy()]
+    for x in ins[1:]:
+        O.reduce_local(op, dt, x, acc)
+        outs.append(acc.copy())
+    return outs
+
+
+@pytest.mark.parametrize("np_", [1, 2, 3, 8, 9, 12, 64])
+@pytest.mark.parametrize("dt", [23, 24, 4, 1, 27, 25])
+def test_prefix_kernel(torch_cuda, np_, dt):
+    torch = torch_cuda
+    for n in (1, 999, (1 << 18) + 5):
+        if np_ > 12 and n > 999:
+            continue
+        ins = [src_of(dt, n, k, n) for k in range(np_)]
+        ref = cpu_prefix(5, dt, ins)
+        di = [to_dev(torch, a) for a in ins]
+        do = [torch.zeros_like(t) for t in di]
+        _lib.prefix(5, dt, [t.data_ptr() for t in do], [t.data_ptr() for t in di], n)
+        torch.cuda.synchronize()
+        for k in range(np_):
+            assert np.array_equal(bits(from_dev(do[k], ref[k])), bits(ref[k])), (np_, n, k)
+
+
+@pytest.mark.parametrize("np_", [3, 8, 12])
+def test_prefix_kernel_aliasing(torch_cuda, np_):
+    """An in-place exscan: output k-1 is input k's buffer.  np <= 8 may alias any input;
+    larger np names the aliased input `own` (one per call)."""
+    torch = torch_cuda
+    dt, n = 24, 4099
+    ins = [src_of(dt, 5, k, n) for k in range(np_)]
+    ref = cpu_prefix(5, dt, ins)
+    j = np_ // 2
+    di = [to_dev(torch, a) for a in ins]
+    do = [torch.zeros_like(t) for t in di]
+    do[j - 1] = di[j]  # output j-1 overwrites input j
+    _lib.prefix(5, dt, [t.data_ptr() for t in do], [t.data_ptr() for t in di], n,
+                own=j if np_ > 8 else -1)
+    torch.cuda.synchronize()
+    for k in range(np_):
+        assert np.array_equal(bits(from_dev(do[k], ref[k])), bits(ref[k])), (np_, k)
+
+
+@pytest.mark.parametrize("P", [9, 12, 16, 64])
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("dt,op", [(23, 5), (11, 2), (27, 6), (4, 4)])
+def test_fold_runtime_p(torch_cuda, P, order, dt, op):
+    torch = torch_cuda
+    n = 1001
+    ins = [O.fill(dt, 1 if op == 6 else 0, 3, k, n) for k in range(P)]
+    ref = plansim.fold_values(op, dt, ins, order)
+    di = [to_dev(torch, a) for a in ins]
+    out = torch.zeros_like(di[0])
+    _lib.fold(op, dt, order, out.data_ptr(), [t.data_ptr() for t in di], n)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(from_dev(out, ref)), bits(ref))
+
+
+def loopback(torch, alg, op, dt, srcs, dsts_init=None, in_place=False, pad=0):
+    P = len(srcs)
+    ds = [to_dev(torch, a, pad) for a in srcs]
+    if in_place:
+        dd = ds
+    elif dsts_init is not None:
+        dd = [to_dev(torch, a, pad) for a in dsts_init]
+    else:
+        dd = [torch.zeros_like(t) for t in ds]
+    S.loopback_allreduce(alg, op, dt, [t.data_ptr() + pad for t in ds],
+                         [t.data_ptr() + pad for t in dd], srcs[0].size)
+    torch.cuda.synchronize()
+    return [from_dev(dd[p], srcs[p], pad) for p in range(P)]
+
+
+@pytest.mark.parametrize("exclusive", [False, True])
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 8, 12])
+@pytest.mark.parametrize("dt", [23, 24, 4, 1, 18, 27, 26, 25])
+def test_loopback_scan(torch_cuda, exclusive, P, dt):
+    torch = torch_cuda
+    alg = _lib.PLAN_EXSCAN if exclusive else _lib.PLAN_INSCAN
+    for n in (1, 7, 4096 + 3, (1 << 20) + 1):
+        if n > 5000 and dt not in (23, 4):
+            continue
+        srcs = [src_of(dt, n, p, n) for p in range(P)]
+        ref = O.scan(5, dt, srcs, exclusive)
+        for in_place, pad in ((False, 0), (True, 0), (False, 4)):
+            got = loopback(torch, alg, 5, dt, srcs, in_place=in_place, pad=pad)
+            for p in range(P):
+                assert np.array_equal(bits(got[p]), bits(ref[p])), (P, n, p, in_place, pad)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8, 9])
+@pytest.mark.parametrize("copy_root", [False, True])
+def test_loopback_bcast(torch_cuda, P, copy_root):
+    torch = torch_cuda
+    rng = np.random.default_rng(P)
+    for nbytes, dt, np_t in ((1, 13, np.uint8), (1000, 13, np.uint8), (65536, 15, np.uint32),
+                             ((4 << 20) + 8, 16, np.uint64), (200001, 13, np.uint8)):
+        n = nbytes // np.dtype(np_t).itemsize
+        for root in sorted({0, P - 1, P // 2}):
+            srcs = [rng.integers(0, 255, n * np.dtype(np_t).itemsize, dtype=np.uint8).view(np_t)
+                    for _ in range(P)]
+            init = [np.full(n, 0x5A, np_t) for _ in range(P)]
+            ref = O.bcast(srcs, root, copy_root, [a.copy() for a in init])
+            got = loopback(torch, _lib.plan_bcast(root, copy_root), 5, dt, srcs, dsts_init=init)
+            for p in range(P):
+                assert np.array_equal(got[p], ref[p]), (P, nbytes, root, p)
+
+
+@pytest.mark.parametrize("alg", ["ring", "recdbl_direct", "recdbl", "rechalving"])
+def test_loopback_reduce_twelve_pes(torch_cuda, alg):
+    """12 PEs: ring / recdbl_direct fold 12 inputs in one runtime-P kernel.  The tree
+    schedules equal SOS recdbl_sw bit for bit for commutative element semantics (fp sum)."""
+    torch = torch_cuda
+    P, dt, op = 12, 23, 5
+    for n in (13, 50001):
+        srcs = [O.fill(dt, 0, n, p, n) for p in range(P)]
+        got = loopback(torch, alg, op, dt, srcs)
+        ref = O.ring(op, dt, srcs) if alg == "ring" else O.recdbl(op, dt, srcs)
+        for p in range(P):
+            assert np.array_equal(bits(got[p]), bits(ref[p])), (alg, n, p)

@@ -61,3 +61,19 @@ def test_team_check(np_):
     # PEs print concurrently, so lines may interleave: count the reports, not lines
     ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
     assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("np_", [2, 3, 4, 8])
+def test_coll_check(np_):
+    """Scans and broadcasts through the public API (tools/coll_check.py)."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "coll_check.py")], timeout=900)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
+    assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("np_", [1, 2, 3, 4, 6])
+def test_team_management(np_):
+    """split_strided / split_2d / team-slot pool / translate / config (tools/team_mgmt_check.py)."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_mgmt_check.py")], timeout=300)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
+    assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
