@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-host", action="store_true", help="skip the host-resident leg")
+    p.add_argument("--no-adjacent", action="store_true",
+                   help="skip the scan/broadcast legs (prefix kernel at N=1, team calls at N>1)")
     p.add_argument("--team", action="store_true",
                    help="run the team (shmem_*_reduce) leg even at WORLD_SIZE 1")
     p.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
@@ -198,6 +200,42 @@ def host_resident(args, torch):
     return out
 
 
+def prefix_kernel(args, torch):
+    """The team scans' local step (sosx_prefix, plan.h PREFIX) at the headline size: P=8
+    input chunks of nreduce/8 elements (one PE's share of an 8-PE scan), 8 outputs.
+    Algorithmic HBM bytes = 2 * P * chunk * sizeof(T).  Reported beside `value`."""
+    from sos_amd import _lib as L
+    dt = L.dtype_id(args.dtype)
+    es = L.dtype_size(dt)
+    P = 8
+    chunk = args.n // P
+    stream = torch.cuda.current_stream()
+    S = stream.cuda_stream
+    ins = [torch.empty(chunk * es, dtype=torch.uint8, device="cuda") for _ in range(P)]
+    outs = [torch.empty_like(x) for x in ins]
+    for k, x in enumerate(ins):
+        L.fill(dt, L.DIST_UNIFORM, SEED, k, x.data_ptr(), chunk, 0, S)
+    ip, op_ = [x.data_ptr() for x in ins], [x.data_ptr() for x in outs]
+    launch = lambda: L.prefix("sum", dt, op_, ip, chunk, -1, S)  # noqa: E731
+    for _ in range(3):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(max(args.steps // 2, 5))]
+    for st_, en in ev:
+        st_.record(stream)
+        launch()
+        en.record(stream)
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in ev)
+    mean_s = sum(ms) / len(ms) / 1e3
+    algo = 2 * P * chunk * es
+    del ins, outs
+    return {"kernel": "sos::k_prefix<NP=8>", "inputs": P, "elements_per_input": chunk,
+            "algorithmic_bytes_per_launch": algo, "mean_kernel_ms": round(mean_s * 1e3, 5),
+            "achieved_GBs": round(algo / mean_s / 1e9, 1),
+            "frac_of_hbm_peak": round(algo / mean_s / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def variants_ab(args, torch, L, launch):
     """Interleaved A/B of every combine variant in one process (guide rule 24)."""
     lib = L.lib()
@@ -332,6 +370,8 @@ def main():
             res["roofline"]["traffic_note"] = str(info)
     if rank == 0 and not args.no_host:
         res["host_resident"] = host_resident(args, torch)
+    if rank == 0 and not args.no_adjacent:
+        res["scan_prefix_kernel"] = prefix_kernel(args, torch)
     if rank == 0 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(res), flush=True)

@@ -108,6 +108,11 @@ def main(args, torch):
         dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
         results[tname] = {"t_step": t_step, "prof": prof, "mismatches": int(mmt.item())}
 
+    adjacent = {}
+    if not getattr(args, "no_adjacent", False):
+        adjacent = adjacent_collectives(args, torch, dist, L, S, dt, es, n, src, dst, stream,
+                                        seed, rank, world)
+
     primary = "rccl" if results["rccl"].get("available", True) else "p2p"
     r = results[primary]
     t_step, prof = r["t_step"], r["prof"]
@@ -160,6 +165,8 @@ def main(args, torch):
     }
     if primary == "rccl" and results["p2p"].get("available", True):
         res["p2p_transport"] = team_roof(results["p2p"])
+    if adjacent:
+        res["adjacent_collectives"] = adjacent
     if rank == 0:
         print(json.dumps(res), flush=True)
     dist.barrier()
@@ -168,6 +175,80 @@ def main(args, torch):
     S.shmem_finalize()
     dist.destroy_process_group()
     return 0
+
+
+def adjacent_collectives(args, torch, dist, L, S, dt, es, n, src, dst, stream, seed, rank, world):
+    """shmemx_<T>_sum_inscan and shmem_<T>_broadcast (root 0) at the bench size, on each
+    transport: time per call (max over ranks), the bytes each PE puts on xGMI, and a
+    bitwise check on fresh inputs (scan: one prefix launch over every PE's regenerated
+    source; broadcast: the root's regenerated source)."""
+    import time as _t
+    team = S.team_world()
+    P = world
+    steps = max(min(args.steps, 10), 2)
+    out = {}
+    scan_fn = getattr(S, f"shmemx_{args.dtype}_sum_inscan", None)
+    bcast_fn = getattr(S, f"shmem_{args.dtype}_broadcast", None)
+    colls = []
+    if scan_fn is not None:
+        colls.append(("inscan", lambda: scan_fn(team, dst, src, n),
+                      2 * (P - 1) / P * n * es))
+    # broadcast: the root puts the payload on its links once (scattered over P-1 links
+    # above 64 KiB); each non-root forwards its 1/(P-1) share to the P-2 others
+    colls.append(("broadcast_root0", lambda: bcast_fn(team, dst, src, n, 0), n * es))
+    for tname, tid in (("rccl", 0), ("p2p", 1)):
+        if S.lib().shmemx_set_transport(tid) < 0:
+            continue
+        for cname, call, wire in colls:
+            for _ in range(2):
+                call()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = _t.perf_counter()
+            for _ in range(steps):
+                call()
+            torch.cuda.synchronize()
+            t1 = _t.perf_counter()
+            dist.barrier()
+            el = torch.tensor([t1 - t0], dtype=torch.float64)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            ts = el.item() / steps
+            # check on fresh inputs
+            cseed = seed + 101 + tid
+            L.fill(dt, L.DIST_UNIFORM, cseed, rank, src, n, 0, stream)
+            torch.cuda.synchronize()
+            dist.barrier()
+            call()
+            if cname == "inscan":
+                ins = []
+                for p in range(P):
+                    b = torch.empty(n * es, dtype=torch.uint8, device="cuda")
+                    L.fill(dt, L.DIST_UNIFORM, cseed, p, b.data_ptr(), n, 0, stream)
+                    ins.append(b)
+                outs = [torch.empty_like(x) for x in ins]
+                L.prefix("sum", dt, [o.data_ptr() for o in outs], [x.data_ptr() for x in ins],
+                         n, -1, stream)
+                exp = outs[rank]
+            else:
+                exp = torch.empty(n * es, dtype=torch.uint8, device="cuda")
+                L.fill(dt, L.DIST_UNIFORM, cseed, 0, exp.data_ptr(), n, 0, stream)
+            torch.cuda.synchronize()
+            mm = L.count_mismatch(exp.data_ptr(), dst, n, es, stream)
+            mmt = torch.tensor([mm], dtype=torch.int64)
+            dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
+            if cname == "inscan":
+                del ins, outs
+            del exp
+            L.fill(dt, L.DIST_UNIFORM, seed, rank, src, n, 0, stream)
+            torch.cuda.synchronize()
+            out.setdefault(tname, {})[cname] = {
+                "ms_per_call": round(ts * 1e3, 4),
+                "payload_GiBs_per_pe": round(n * es / ts / GiB, 3),
+                "wire_bytes_per_pe": int(wire),
+                "wire_GBs_per_pe": round(wire / ts / 1e9, 1),
+                "bitwise_mismatches_all_ranks": int(mmt.item())}
+    S.lib().shmemx_set_transport(0)
+    return out
 
 
 def self_check(torch, L, S, dt, opid, dist_kind, seed, world, n, es, alg, dst, stream):
