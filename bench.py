@@ -60,6 +60,10 @@ def parse():
                    help="skip the scan/broadcast legs (prefix kernel at N=1, team calls at N>1)")
     p.add_argument("--team", action="store_true",
                    help="run the team (shmem_*_reduce) leg even at WORLD_SIZE 1")
+    p.add_argument("--sweep", action="store_true",
+                   help="SURVEY 8(d) config #5 roofline scan of the combine kernel instead of "
+                        "the headline line (N=1)")
+    p.add_argument("--sweep-max", type=int, default=256 << 20)
     p.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args()
     a.n = a.nreduce
@@ -277,6 +281,78 @@ def variants_ab(args, torch, L, launch):
     log(f"{'calib: D2D copy':>18} {ms:10.4f} {'':9} {2 * args.n * es / (ms / 1e3) / 1e9:20.1f}")
 
 
+# config #5 (and #2, #3): (type, op) pairs of the roofline scan
+SWEEP_PAIRS = [("int", "min"), ("int", "max"), ("int", "prod"),
+               ("double", "min"), ("double", "max"), ("double", "prod"), ("double", "sum"),
+               ("complexd", "prod"), ("complexd", "sum"),
+               ("int64", "and"), ("int64", "or"), ("int64", "xor"),
+               ("float", "sum")]
+
+
+def sweep(args, torch):
+    """Roofline scan of the local combine (sosx_combine) over nreduce = 1Ki * 4^k up to
+    --sweep-max for every (type, op) of SURVEY 8(d) configs #2, #3 and #5.  Per point:
+    the mean HIP-event kernel time over a batch of launches, algorithmic HBM GB/s
+    (3 * n * sizeof(T) per launch) and its fraction of the 8 TB/s peak, and the host
+    wall time per call (launch-bound at small n).  Parity at these sizes is
+    tests/test_gpu_configs.py (bit-exact vs the oracle); here each point is checked
+    against the fused fold kernel run on the same two inputs (an independent code path,
+    sosx_fold with 2 inputs)."""
+    from sos_amd import _lib as L
+    stream = torch.cuda.current_stream()
+    S = stream.cuda_stream
+    sizes = []
+    n = 1 << 10
+    while n <= args.sweep_max:
+        sizes.append(n)
+        n *= 4
+    rows = []
+    for tname, oname in SWEEP_PAIRS:
+        dt, op = L.dtype_id(tname), L.op_id(oname)
+        es = L.dtype_size(dt)
+        dist = L.DIST_PROD if oname == "prod" else L.DIST_UNIFORM
+        nmax = sizes[-1]
+        a = torch.empty(nmax * es, dtype=torch.uint8, device="cuda")
+        b = torch.empty_like(a)
+        c = torch.empty_like(a)
+        for n in sizes:
+            L.fill(dt, dist, SEED, 0, a.data_ptr(), n, 0, S)
+            L.fill(dt, dist, SEED, 1, b.data_ptr(), n, 0, S)
+            # check first: fold(a, b) -> c, then combine a OP= b, compare
+            L.fold(op, dt, L.ORDER_LINEAR, c.data_ptr(), [a.data_ptr(), b.data_ptr()], n, S)
+            L.combine(op, dt, a.data_ptr(), b.data_ptr(), n, S)
+            bad = L.count_mismatch(a.data_ptr(), c.data_ptr(), n, es, S)
+            reps = max(5, min(200, int(2e9 // (3 * n * es))))
+            launch = lambda: L.combine(op, dt, a.data_ptr(), b.data_ptr(), n, S)  # noqa: E731
+            for _ in range(3):
+                launch()
+            torch.cuda.synchronize()
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            s0.record(stream)
+            for _ in range(reps):
+                launch()
+            s1.record(stream)
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - t0) / reps
+            kern = s0.elapsed_time(s1) / 1e3 / reps
+            algo = 3 * n * es
+            rows.append({"type": tname, "op": oname, "nreduce": n, "bytes_per_launch": algo,
+                         "kernel_us": round(kern * 1e6, 3), "call_us": round(wall * 1e6, 3),
+                         "GBs": round(algo / kern / 1e9, 1),
+                         "frac_hbm": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4),
+                         "payload_GiBs": round(n * es / kern / GiB, 2),
+                         "check_mismatches": int(bad)})
+            log(f"{tname:>8} {oname:>4} n={n:>10} {kern * 1e6:10.2f} us "
+                f"{algo / kern / 1e9:8.1f} GB/s  frac {algo / kern / 1e9 / HBM_PEAK_GBS:.3f}"
+                f"  check {bad}")
+        del a, b, c
+    return {"sweep": "combine roofline scan, SURVEY 8(d) configs #2/#3/#5, 1 GPU",
+            "peak_GBs": HBM_PEAK_GBS, "kernel": "sos::k_combine3 (sosx_combine)",
+            "timing": "HIP events around a batch of back-to-back launches on one stream",
+            "rows": rows}
+
+
 # ----------------------------------------------------------------------------------
 # PMC traffic: rocprofv3 --pmc pass(es) over a child run of this script
 # ----------------------------------------------------------------------------------
@@ -357,6 +433,9 @@ def main():
         from sos_amd import team_bench
         return team_bench.main(args, torch)
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    if args.sweep:
+        print(json.dumps(sweep(args, torch)), flush=True)
+        return 0
     res = run_combine(args, torch)
     if res is None:
         return 0

@@ -7,7 +7,7 @@
  *                           can run on without host staging.
  *   shmemx_malloc_device    collective symmetric allocation in HBM.
  *   shmemx_reduce_local     the local combine (shmem_internal_reduce_local,
- *                           src/shmem_internal_op.h:305-339) on device memory.
+ *                           src/shmem_internal_op.h:305-339) on HBM or host operands.
  *   shmemx_init_attr /      bootstrap with an RCCL unique id obtained out of band
  *   shmemx_get_unique_id    (e.g. broadcast by torch.distributed), instead of the
  *                           built-in TCP bootstrap of shmem_init().
@@ -46,8 +46,12 @@ SHMEM_FUNCTION_ATTRIBUTES void shmemx_set_stream(void *hip_stream);
 SHMEM_FUNCTION_ATTRIBUTES void *shmemx_get_stream(void);
 SHMEM_FUNCTION_ATTRIBUTES int shmemx_get_device(void);
 
-/* inout[i] = inout[i] OP in[i] on device memory; op/datatype are SOS's internal
- * enums (SOSX_OP_*, SOSX_DT_*).  Asynchronous on the library stream. */
+/* inout[i] = inout[i] OP in[i]; op/datatype are SOS's internal enums (SOSX_OP_*,
+ * SOSX_DT_*).  Either operand may be in HBM or host memory (pageable or pinned):
+ * both in HBM -> one kernel; both on the host -> the H2D || combine || D2H chunk
+ * pipeline; mixed -> the host operand is staged through HBM (the kernel never
+ * dereferences host memory).  Completion: every path returns after the result is
+ * in `inout`, as SOS's CPU loop does.  Returns SOSX_OK or a negative SOSX_ERR_*. */
 SHMEM_FUNCTION_ATTRIBUTES int shmemx_reduce_local(int op, int datatype, size_t count,
                                                   const void *in, void *inout);
 

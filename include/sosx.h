@@ -101,10 +101,14 @@ int sosx_check_op(int op, int dtype);
 int sosx_combine(int op, int dtype, void *inout, const void *in, size_t count, void *stream);
 
 /* The same combine on HOST-resident operands (SOS's symmetric heap is host memory),
- * pipelined H2D || combine || D2H in chunks of `chunk_bytes` (0 = 16 MiB) over three
- * streams; pinned memory overlaps fully.  Synchronous. */
+ * pipelined H2D || combine || D2H in chunks of `chunk_bytes` (0 = 16 MiB pinned,
+ * 64 MiB pageable) over three streams; pinned memory overlaps fully.  Synchronous.
+ * The pipeline keeps 6 chunk-sized HBM slots between calls. */
 int sosx_combine_host(int op, int dtype, void *inout, const void *in, size_t count,
                       size_t chunk_bytes);
+
+/* Frees the host pipeline's HBM slots and streams (shmem_finalize calls it). */
+void sosx_combine_host_release(void);
 
 /* out[i] = a[i] OP b[i]; `out` may alias `a` (then this is sosx_combine). */
 int sosx_combine3(int op, int dtype, void *out, const void *a, const void *b, size_t count,

@@ -81,8 +81,34 @@ _SIGS = {
 }
 
 
+_RUNTIME_LIBS = ("libamdhip64", "libhsa-runtime64", "librccl", "librocm_smi64")
+
+
+def loaded_runtimes():
+    """{runtime library stem: sorted distinct paths mapped into this process}."""
+    found = {k: set() for k in _RUNTIME_LIBS}
+    with open("/proc/self/maps") as f:
+        for line in f:
+            path = line.split()[-1]
+            base = os.path.basename(path)
+            for k in _RUNTIME_LIBS:
+                if base.startswith(k + ".so"):
+                    found[k].add(path)
+    return {k: sorted(v) for k, v in found.items()}
+
+
 def lib():
-    """Load libsos_amd.so (once) and declare its C signatures."""
+    """Load libsos_amd.so (once) and declare its C signatures.
+
+    One HIP runtime per process: torch (when installed) is imported first, so the
+    libamdhip64.so.7 / librccl.so.1 it has already mapped satisfy libsos_amd.so's
+    DT_NEEDED entries by SONAME.  Loaded the other way round, the loader maps
+    /opt/rocm's runtime for libsos_amd.so and torch then maps its own bundled copy
+    (it asks for the unversioned names); the two librocm_smi64 copies then free one
+    static object twice at exit ("double free or corruption").  A second copy that
+    this load maps is refused here rather than left to abort at exit.  (A profiler may
+    have preloaded its own HSA runtime before torch; that copy is not ours to refuse.)
+    """
     global _LIB
     if _LIB is not None:
         return _LIB
@@ -90,7 +116,16 @@ def lib():
         raise ImportError(
             f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback for the SOS reduction path)")
+    try:
+        import torch  # noqa: F401  (maps torch's HIP runtime before ours is resolved)
+    except ImportError:
+        pass
+    before = loaded_runtimes()
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    added = {k: v for k, v in loaded_runtimes().items() if len(v) > max(1, len(before[k]))}
+    if added:
+        raise ImportError(f"loading {LIB_PATH} mapped a second copy of a ROCm runtime "
+                          f"library: {added}")
     for name, (res, args) in _SIGS.items():
         fn = getattr(L, name, None)
         if fn is None:

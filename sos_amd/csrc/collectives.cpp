@@ -470,10 +470,33 @@ int sos_api_scan(shmem_team_t team, void *dest, const void *source, size_t nelem
 int shmemx_reduce_local(int op, int datatype, size_t count, const void *in, void *inout)
 {
     check_initialized("shmemx_reduce_local");
-    // host operands (the SOS heap): pipelined over PCIe; device operands: one kernel
-    if (!is_device_ptr(inout) && !is_device_ptr(in))
-        return sosx_combine_host(op, datatype, inout, in, count, 0);
-    return sosx_combine(op, datatype, inout, in, count, st().stream);
+    // One completion rule for every residency, as SOS's CPU loop: the result is in
+    // `inout` when the call returns.
+    int rc = sos_check_op(op, datatype);
+    if (rc || count == 0) return rc;
+    if (!inout || !in) return SOSX_ERR_ARG;
+    const bool dev_io = is_device_ptr(inout), dev_in = is_device_ptr(in);
+    // both on the host (the SOS heap): H2D || combine || D2H pipeline, synchronous
+    if (!dev_io && !dev_in) return sosx_combine_host(op, datatype, inout, in, count, 0);
+    State &s = st();
+    if (dev_io && dev_in) {
+        rc = sosx_combine(op, datatype, inout, in, count, s.stream);
+    } else {
+        // mixed residency: the kernel never dereferences host memory; the host operand
+        // is staged through HBM (and `inout` copied back when it is the host one)
+        const size_t bytes = count * sosx_dtype_size(datatype);
+        void *d = stage(bytes);
+        if (hipMemcpyAsync(d, dev_io ? in : inout, bytes, hipMemcpyHostToDevice, s.stream) !=
+            hipSuccess)
+            return SOSX_ERR_HIP;
+        rc = dev_io ? sosx_combine(op, datatype, inout, d, count, s.stream)
+                    : sosx_combine(op, datatype, d, in, count, s.stream);
+        if (!rc && !dev_io &&
+            hipMemcpyAsync(inout, d, bytes, hipMemcpyDeviceToHost, s.stream) != hipSuccess)
+            return SOSX_ERR_HIP;
+    }
+    if (rc) return rc;
+    return hipStreamSynchronize(s.stream) == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
 }
 
 // ---- phase timing -----------------------------------------------------------------

@@ -18,7 +18,7 @@ namespace sos {
 // out = a OP b (out may alias a): the local combine.
 // ---------------------------------------------------------------------------------
 template <class T, class OP, int U, bool NTL, bool NTS>
-__global__ __launch_bounds__(kThreads) void k_combine3(T *__restrict__ out, const T *a,
+__global__ __launch_bounds__(kThreads) void k_combine3(T *out, const T *a,
                                                          const T *b, Geom g)
 {
     constexpr int V = Pack<T>::N;
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(kThreads) void k_combine3(T *__restrict__ out, cons
 // bits (gfx950 aux: sc0 = 1, nt = 2, sc1 = 16), one wave-uniform descriptor per tile.
 // Tuning variants only (bench --variants).
 template <class T, class OP, int U, int AUXL, int AUXS>
-__global__ __launch_bounds__(kThreads) void k_combine3_buf(T *__restrict__ out, const T *a,
+__global__ __launch_bounds__(kThreads) void k_combine3_buf(T *out, const T *a,
                                                              const T *b, Geom g)
 {
     constexpr int V = Pack<T>::N;
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(kThreads) void k_combine3_buf(T *__restrict__ out, 
 // alternative (bench --variants); for a pure 3-stream combine the LDS round trip
 // buys nothing over register staging (MI355X guide, "glds vs register staging").
 template <class T, class OP, int U>
-__global__ __launch_bounds__(kThreads) void k_combine3_lds(T *__restrict__ out, const T *a,
+__global__ __launch_bounds__(kThreads) void k_combine3_lds(T *out, const T *a,
                                                              const T *b, Geom g)
 {
     constexpr int V = Pack<T>::N;
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kThreads) void k_combine3_lds(T *__restrict__ out, 
 
 // Relative misalignment between the operands (not 16-B congruent): element loads.
 template <class T, class OP>
-__global__ __launch_bounds__(kThreads) void k_combine3_scalar(T *__restrict__ out, const T *a,
+__global__ __launch_bounds__(kThreads) void k_combine3_scalar(T *out, const T *a,
                                                                 const T *b, size_t n)
 {
     const size_t stride = (size_t)gridDim.x * kThreads;

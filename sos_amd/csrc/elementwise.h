@@ -216,8 +216,16 @@ __device__ __forceinline__ u32x4 ldv(const u32x4 *p)
 template <bool NT>
 __device__ __forceinline__ void stv(u32x4 *p, u32x4 v)
 {
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
+    if constexpr (NT) {
+        // The empty asm pins the value first: without it LLVM drops the !nontemporal
+        // of this store when the value comes out of select chains (fp64/complex SUM/PROD
+        // with the x86 NaN rule), leaving a cached store and ~12 % less HBM rate at
+        // large n (profiles/r2_sweep.json).
+        asm volatile("" : "+v"(v));
+        __builtin_nontemporal_store(v, p);
+    } else {
+        *p = v;
+    }
 }
 
 constexpr int kThreads = 256;

@@ -70,7 +70,7 @@ __device__ __forceinline__ u32x4 fold_pack(const u32x4 (&x)[NP])
 }
 
 template <class T, class OP, int NP, int ORDER, int U>
-__global__ __launch_bounds__(kThreads) void k_fold(T *__restrict__ out, FoldPtrs ins, Geom g)
+__global__ __launch_bounds__(kThreads) void k_fold(T *out, FoldPtrs ins, Geom g)
 {
     constexpr int V = Pack<T>::N;
     u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kThreads) void k_fold(T *__restrict__ out, FoldPtrs
 }
 
 template <class T, class OP, int NP, int ORDER>
-__global__ __launch_bounds__(kThreads) void k_fold_scalar(T *__restrict__ out, FoldPtrs ins,
+__global__ __launch_bounds__(kThreads) void k_fold_scalar(T *out, FoldPtrs ins,
                                                             size_t n)
 {
     const size_t stride = (size_t)gridDim.x * kThreads;
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kThreads) void k_fold_scalar(T *__restrict__ out, F
 // loads; the TREE order walks the recdbl_sw leaves left to right with a binary-counter
 // stack (merge equal-height neighbours: w[k] = w[k] OP w[k+d]), so no P-sized array.
 template <class T, class OP, int ORDER>
-__global__ __launch_bounds__(kThreads) void k_fold_dyn(T *__restrict__ out, FoldPtrs ins, int np,
+__global__ __launch_bounds__(kThreads) void k_fold_dyn(T *out, FoldPtrs ins, int np,
                                                          size_t n)
 {
     const size_t stride = (size_t)gridDim.x * kThreads;

@@ -23,10 +23,34 @@ struct Pipe {
     void *a[kSlots] = {nullptr, nullptr, nullptr};
     void *b[kSlots] = {nullptr, nullptr, nullptr};
     size_t slot_bytes = 0;
-    hipEvent_t in_done[kSlots], cmp_done[kSlots], out_done[kSlots];
+    hipEvent_t in_done[kSlots] = {}, cmp_done[kSlots] = {}, out_done[kSlots] = {};
 };
 
 Pipe g_pipe;
+
+// Frees everything the pipe holds (slots, events, streams) and marks it not ready, so
+// a failed or stale setup can never leave freed slots behind a valid-looking size.
+void release()
+{
+    Pipe &p = g_pipe;
+    if (p.ready || p.s_in || p.s_cmp || p.s_out) (void)hipDeviceSynchronize();
+    for (int i = 0; i < Pipe::kSlots; ++i) {
+        if (p.a[i]) (void)hipFree(p.a[i]);
+        if (p.b[i]) (void)hipFree(p.b[i]);
+        p.a[i] = p.b[i] = nullptr;
+        if (p.in_done[i]) (void)hipEventDestroy(p.in_done[i]);
+        if (p.cmp_done[i]) (void)hipEventDestroy(p.cmp_done[i]);
+        if (p.out_done[i]) (void)hipEventDestroy(p.out_done[i]);
+        p.in_done[i] = p.cmp_done[i] = p.out_done[i] = nullptr;
+    }
+    for (hipStream_t *s : {&p.s_in, &p.s_cmp, &p.s_out}) {
+        if (*s) (void)hipStreamDestroy(*s);
+        *s = nullptr;
+    }
+    p.slot_bytes = 0;
+    p.device = -1;
+    p.ready = false;
+}
 
 int setup(size_t slot_bytes)
 {
@@ -34,29 +58,37 @@ int setup(size_t slot_bytes)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return SOSX_ERR_HIP;
     if (p.ready && p.device == dev && p.slot_bytes >= slot_bytes) return SOSX_OK;
-    if (p.ready) {
-        (void)hipDeviceSynchronize();
-        for (int i = 0; i < Pipe::kSlots; ++i) {
-            (void)hipFree(p.a[i]);
-            (void)hipFree(p.b[i]);
+    if (p.ready && p.device != dev) release();  // streams/events belong to the old device
+    if (!p.ready) {
+        bool ok = hipStreamCreateWithFlags(&p.s_in, hipStreamNonBlocking) == hipSuccess &&
+                  hipStreamCreateWithFlags(&p.s_cmp, hipStreamNonBlocking) == hipSuccess &&
+                  hipStreamCreateWithFlags(&p.s_out, hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; ok && i < Pipe::kSlots; ++i)
+            ok = hipEventCreateWithFlags(&p.in_done[i], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&p.cmp_done[i], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&p.out_done[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            release();
+            return SOSX_ERR_HIP;
         }
-    } else {
-        if (hipStreamCreateWithFlags(&p.s_in, hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&p.s_cmp, hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&p.s_out, hipStreamNonBlocking) != hipSuccess)
-            return SOSX_ERR_HIP;
-        for (int i = 0; i < Pipe::kSlots; ++i)
-            if (hipEventCreateWithFlags(&p.in_done[i], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&p.cmp_done[i], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&p.out_done[i], hipEventDisableTiming) != hipSuccess)
-                return SOSX_ERR_HIP;
+        p.device = dev;
+        p.ready = true;
     }
+    // grow the slots: free the old ones first (HBM headroom); any failure releases all
+    (void)hipDeviceSynchronize();
+    for (int i = 0; i < Pipe::kSlots; ++i) {
+        if (p.a[i]) (void)hipFree(p.a[i]);
+        if (p.b[i]) (void)hipFree(p.b[i]);
+        p.a[i] = p.b[i] = nullptr;
+    }
+    p.slot_bytes = 0;
     for (int i = 0; i < Pipe::kSlots; ++i)
-        if (hipMalloc(&p.a[i], slot_bytes) != hipSuccess || hipMalloc(&p.b[i], slot_bytes) != hipSuccess)
+        if (hipMalloc(&p.a[i], slot_bytes) != hipSuccess || hipMalloc(&p.b[i], slot_bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            release();
             return SOSX_ERR_HIP;
+        }
     p.slot_bytes = slot_bytes;
-    p.device = dev;
-    p.ready = true;
     return SOSX_OK;
 }
 
@@ -81,7 +113,7 @@ int sosx_combine_host(int op, int dtype, void *inout, const void *in, size_t cou
         const bool pinned = hipPointerGetAttributes(&at, inout) == hipSuccess &&
                             at.type == hipMemoryTypeHost;
         if (!pinned) (void)hipGetLastError();
-        chunk_bytes = pinned ? (16u << 20) : (256u << 20);
+        chunk_bytes = pinned ? (16u << 20) : (64u << 20);
     }
     size_t chunk = chunk_bytes / ts;
     if (chunk == 0) chunk = 1;
@@ -113,5 +145,9 @@ int sosx_combine_host(int op, int dtype, void *inout, const void *in, size_t cou
     }
     return hipStreamSynchronize(p.s_out) == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
 }
+
+// Returns the pipeline's device slots (6 x chunk bytes of HBM) and streams; called by
+// shmem_finalize.  The next sosx_combine_host sets them up again.
+void sosx_combine_host_release(void) { release(); }
 
 }  // extern "C"

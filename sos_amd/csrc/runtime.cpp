@@ -542,6 +542,7 @@ void shmem_finalize(void)
     s.scratch = s.stage = nullptr;
     s.scratch_bytes = s.stage_bytes = 0;
     s.dbar = nullptr;
+    sosx_combine_host_release();
     if (s.host_heap.base) (void)hipHostFree(s.host_heap.base);
     for (size_t q = 0; q < s.peer_heap.size(); ++q)
         if ((int)q != s.my_pe && s.peer_heap[q]) (void)hipIpcCloseMemHandle(s.peer_heap[q]);
@@ -855,23 +856,72 @@ int shmem_team_translate_pe(shmem_team_t src_team, int src_pe, shmem_team_t dest
     return idx < d->size ? idx : -1;
 }
 
+// All-gather of one 64-bit word per member of team `t` over RCCL (the path without node
+// shared memory, e.g. shmemx_init_attr): grouped ncclSend/ncclRecv with every other
+// member, one word each way.  Collective over `t`; returns the words in team order.
+static std::vector<uint64_t> team_allgather_word(const Team &t, uint64_t mine)
+{
+    State &s = st();
+    std::vector<uint64_t> out((size_t)t.size, 0);
+    out[(size_t)t.my_idx] = mine;
+    if (t.size <= 1) return out;
+    uint64_t *d = nullptr;
+    hip_check(hipMalloc(&d, (size_t)t.size * sizeof(uint64_t)), "hipMalloc(team words)");
+    hip_check(hipMemcpyAsync(d + t.my_idx, &mine, sizeof mine, hipMemcpyHostToDevice, s.stream),
+              "team words H2D");
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int i = 0; i < t.size; ++i) {
+        if (i == t.my_idx) continue;
+        nccl_check(ncclSend(d + t.my_idx, sizeof mine, ncclUint8, t.world_rank(i), s.comm, s.stream),
+                   "ncclSend(team words)");
+        nccl_check(ncclRecv(d + i, sizeof mine, ncclUint8, t.world_rank(i), s.comm, s.stream),
+                   "ncclRecv(team words)");
+    }
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    hip_check(hipMemcpyAsync(out.data(), d, out.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                             s.stream), "team words D2H");
+    hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize(team words)");
+    hip_check(hipFree(d), "hipFree(team words)");
+    return out;
+}
+
 // Team creation agreement over the parent (src/shmem_team.c:354-432): the members AND
 // their free-slot masks and take the lowest common slot; every parent PE then returns
-// the MAX of the members' status, so all agree.  Node shared memory carries the words.
+// the MAX of the members' status, so all agree.  Node shared memory carries the words;
+// without it (shmemx_init_attr) they are all-gathered over RCCL.
 static int team_agree_slot(const Team &parent, const Team &child, bool member, int *slot)
 {
     State &s = st();
-    const bool shm = parent.size > 1 && s.shm.extra;
-    const int me_world = s.my_pe;
     *slot = -1;
-    if (shm) {
-        team_word_put(0, me_world, member ? s.team_avail : 0);
-        team_barrier(parent);
+    if (parent.size <= 1 || !s.shm.extra) {
+        // non-members contribute all ones, the neutral word of the AND
+        uint64_t all = s.team_avail;
+        if (parent.size > 1)
+            for (uint64_t w : team_allgather_word(parent, member ? s.team_avail : ~0ull)) all &= w;
+        int status = 0;
+        if (member) {
+            const int idx = all ? __builtin_ctzll(all) : -1;
+            if (idx < 0 || idx >= s.teams_max) {
+                warn("No more teams available (max = %ld), try increasing SHMEM_TEAMS_MAX",
+                     s.teams_max);
+                status = 1;
+            } else {
+                *slot = idx;
+            }
+        }
+        if (parent.size <= 1) return status;
+        int agreed = 0;
+        for (uint64_t w : team_allgather_word(parent, (uint64_t)status))
+            agreed = std::max(agreed, (int)w);
+        return agreed;
     }
+    const int me_world = s.my_pe;
+    team_word_put(0, me_world, member ? s.team_avail : 0);
+    team_barrier(parent);
     int status = 0;
     if (member) {
         uint64_t all = s.team_avail;
-        for (int i = 0; shm && i < child.size; ++i) all &= team_word_get(0, child.world_rank(i));
+        for (int i = 0; i < child.size; ++i) all &= team_word_get(0, child.world_rank(i));
         const int idx = all ? __builtin_ctzll(all) : -1;
         if (idx < 0 || idx >= s.teams_max) {
             warn("No more teams available (max = %ld), try increasing SHMEM_TEAMS_MAX", s.teams_max);
@@ -880,7 +930,6 @@ static int team_agree_slot(const Team &parent, const Team &child, bool member, i
             *slot = idx;
         }
     }
-    if (!shm) return status;
     team_word_put(1, me_world, (uint64_t)status);
     team_barrier(parent);
     int agreed = 0;

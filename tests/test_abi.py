@@ -140,3 +140,19 @@ def test_combine_status_codes_without_gpu():
     assert L.sosx_check_op(5, 25) == 0      # long double is valid in SOS ...
     assert L.sosx_combine(5, 25, None, None, 0, None) == 0   # ... (count 0: nothing to do)
     assert L.sosx_dtype_size(27) == 16 and L.sosx_dtype_size(25) == 16
+
+
+@pytest.mark.parametrize("order", ["lib_then_torch", "torch_then_lib"])
+def test_one_hip_runtime_per_process(order):
+    """libsos_amd.so and torch share ONE HIP runtime whatever the import order (two copies
+    made the process abort at exit: "double free or corruption")."""
+    first, second = (("from sos_amd import _lib; _lib.lib()", "import torch")
+                     if order == "lib_then_torch" else
+                     ("import torch", "from sos_amd import _lib; _lib.lib()"))
+    code = (f"import sys; sys.path.insert(0, {ROOT!r})\n{first}\n{second}\n"
+            "from sos_amd import _lib\n"
+            "dup = {k: v for k, v in _lib.loaded_runtimes().items() if len(v) > 1}\n"
+            "assert not dup, dup\nprint('one runtime')\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "one runtime" in r.stdout

@@ -7,6 +7,8 @@ Every result is compared bit for bit with the CPU oracle (oracle/sos_oracle.c):
   sosx_fold with 9..64 inputs == the plan simulator's LINEAR / TREE fold
   loopback ring over 12 PEs   == oracle_ring   (src/collectives.c:647-764)
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -99,6 +101,19 @@ def test_fold_runtime_p(torch_cuda, P, order, dt, op):
     _lib.fold(op, dt, order, out.data_ptr(), [t.data_ptr() for t in di], n)
     torch.cuda.synchronize()
     assert np.array_equal(bits(from_dev(out, ref)), bits(ref))
+
+
+def test_fold_selection_exits_cleanly():
+    """The float-sum runtime-P fold selection used to abort at interpreter exit (two HIP
+    runtimes in one process); the selection must now exit with status 0."""
+    import subprocess
+    import sys
+    here = os.path.abspath(__file__)
+    r = subprocess.run([sys.executable, "-m", "pytest", here, "-q", "-p", "no:cacheprovider",
+                        "-k", "test_fold_runtime_p and 23-5"], capture_output=True, text=True,
+                       timeout=110, cwd=os.path.dirname(os.path.dirname(here)))
+    assert r.returncode == 0, (r.stdout[-1500:], r.stderr[-1500:])
+    assert "8 passed" in r.stdout
 
 
 def loopback(torch, alg, op, dt, srcs, dsts_init=None, in_place=False, pad=0):

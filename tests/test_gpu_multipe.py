@@ -77,3 +77,32 @@ def test_team_management(np_):
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_mgmt_check.py")], timeout=300)
     ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
     assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("np_", [2, 4])
+def test_bench_team_leg(np_):
+    """The driver's N > 1 bench path (torch.distributed.run -> bench.py -> team_bench) with
+    np_ ranks on this one GPU over the p2p transport: one JSON line whose bitwise self-check
+    and adjacent-collective checks are clean on every rank.  (The RCCL leg needs one GPU
+    per rank; it reports itself unavailable here.)"""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update({"SHMEMX_TRANSPORT": "p2p", "SHMEMX_DEVICE": "0", "PYTHONPATH": ROOT})
+    port = 29400 + np_ * 7 + os.getpid() % 500
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        f"--nproc-per-node={np_}", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", str(np_), "--steps", "3", "--warmup", "1",
+                        "--nreduce", str((1 << 20) + 3)],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    import json
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == np_ and res["value"] > 0
+    assert res["config"]["transport"] == "p2p"
+    assert res["check"]["bitwise_mismatches_all_ranks"] == 0
+    for coll in res.get("adjacent_collectives", {}).get("p2p", {}).values():
+        assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]

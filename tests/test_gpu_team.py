@@ -128,6 +128,31 @@ def test_reduce_local_extension(torch_cuda, shmem1, oracle):
     assert np.array_equal(da.cpu().numpy().view(np.uint64), ref.view(np.uint64))
 
 
+@pytest.mark.parametrize("where", ["dev_inout_host_in", "host_inout_dev_in", "host_both"])
+def test_reduce_local_mixed_residency(torch_cuda, shmem1, oracle, where):
+    """Pageable host operands next to HBM ones: the host side is staged, never dereferenced
+    by the kernel, and every path has completed when the call returns (no synchronize)."""
+    S, torch = shmem1, torch_cuda
+    n = (1 << 18) + 7
+    a, b = oracle.fill(23, 0, 9, 0, n), oracle.fill(23, 0, 9, 1, n)
+    ref = a.copy()
+    oracle.reduce_local(5, 23, b, ref)
+    io_h, in_h = a.copy(), b.copy()  # numpy = pageable malloc memory
+    io_d, in_d = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    torch.cuda.synchronize()
+    if where == "dev_inout_host_in":
+        assert S.shmemx_reduce_local(5, 23, n, in_h.ctypes.data, io_d.data_ptr()) == 0
+        got = io_d.cpu().numpy()
+    elif where == "host_inout_dev_in":
+        assert S.shmemx_reduce_local(5, 23, n, in_d.data_ptr(), io_h.ctypes.data) == 0
+        got = io_h  # read straight away: the call is synchronous
+    else:
+        assert S.shmemx_reduce_local(5, 23, n, in_h.ctypes.data, io_h.ctypes.data) == 0
+        got = io_h
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(in_h.view(np.uint32), b.view(np.uint32))  # `in` left untouched
+
+
 def _run(cmd, timeout=120, env=None):
     e = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):

@@ -18,7 +18,7 @@ run() {  # name seconds cmd...
 }
 R=$(pwd)
 # 1. headline combine, kernel trace + stats
-run combine_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$out/combine" -o combine -- python3 bench.py --no-pmc --no-cpu --steps 50
+run combine_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$out/combine" -o combine -- python3 bench.py --no-pmc --no-cpu --no-host --no-adjacent --steps 50
 # 2. PMC passes (one counter group per pass)
 run combine_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/$out/fetch" -o fetch -- python3 bench.py --child-pmc --steps 5 --warmup 1
 run combine_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/$out/write" -o write -- python3 bench.py --child-pmc --steps 5 --warmup 1
