@@ -63,7 +63,10 @@ def parse():
     p.add_argument("--sweep", action="store_true",
                    help="SURVEY 8(d) config #5 roofline scan of the combine kernel instead of "
                         "the headline line (N=1)")
-    p.add_argument("--sweep-max", type=int, default=256 << 20)
+    p.add_argument("--sweep-max", type=int, default=256 << 20,
+                   help="largest nreduce of the N=1 sweep and of the N>1 size curve")
+    p.add_argument("--no-team-sweep", action="store_true",
+                   help="N>1: skip the nreduce 1Mi..256Mi size curve")
     p.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args()
     a.n = a.nreduce

@@ -43,7 +43,11 @@ def main(args, torch):
     es = L.dtype_size(dt)
     n = args.n
     os.environ.setdefault("SHMEMX_TRANSPORT", "both")
-    os.environ.setdefault("SHMEMX_DEVICE_HEAP_SIZE", str(2 * n * es + (320 << 20)))
+    sweep_sizes = [] if getattr(args, "no_team_sweep", False) else \
+        [m for m in (1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20)
+         if m != n and m <= getattr(args, "sweep_max", 256 << 20)]
+    nmax = max([n] + sweep_sizes)
+    os.environ.setdefault("SHMEMX_DEVICE_HEAP_SIZE", str(2 * nmax * es + (320 << 20)))
     os.environ.setdefault("SHMEMX_STAGE_BYTES", str(64 << 20))
     os.environ.setdefault("SHMEMX_DEVICE", str(local))
     dist.init_process_group("gloo")
@@ -55,9 +59,9 @@ def main(args, torch):
     dist_kind = L.DIST_PROD if args.op == "prod" else L.DIST_UNIFORM
     seed = 0x5EED
     stream = S.lib().shmemx_get_stream()
-    src = S.shmemx_malloc_device(n * es)
-    dst = S.shmemx_malloc_device(n * es)
-    L.fill(dt, dist_kind, seed, rank, src, n, 0, stream)
+    src = S.shmemx_malloc_device(nmax * es)
+    dst = S.shmemx_malloc_device(nmax * es)
+    L.fill(dt, dist_kind, seed, rank, src, nmax, 0, stream)
     torch.cuda.synchronize()
     fn = getattr(S, f"shmem_{args.dtype}_{args.op}_reduce")
     team = S.team_world()
@@ -107,6 +111,9 @@ def main(args, torch):
         mmt = torch.tensor([mm], dtype=torch.int64)
         dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
         results[tname] = {"t_step": t_step, "prof": prof, "mismatches": int(mmt.item())}
+
+    curve = size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
+                       src, dst, stream, sorted(sweep_sizes + [n]), results) if sweep_sizes else {}
 
     adjacent = {}
     if not getattr(args, "no_adjacent", False):
@@ -165,6 +172,8 @@ def main(args, torch):
     }
     if primary == "rccl" and results["p2p"].get("available", True):
         res["p2p_transport"] = team_roof(results["p2p"])
+    if curve:
+        res["size_curve"] = curve
     if adjacent:
         res["adjacent_collectives"] = adjacent
     if rank == 0:
@@ -175,6 +184,63 @@ def main(args, torch):
     S.shmem_finalize()
     dist.destroy_process_group()
     return 0
+
+
+def size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world, src, dst,
+               stream, sizes, headline):
+    """The team reduction over nreduce = 1Mi .. 256Mi (SURVEY 8(d) config #5 / the north
+    star's 1->8-GPU curve) on each transport: whole-job GiB/s (world * n * s / t, max over
+    ranks), busbw = 2(P-1)/P * n * s / t and its fraction of one xGMI link and of all 7.
+    The largest size also gets the bitwise self-check on fresh inputs."""
+    P = world
+    out = {}
+    alg = L.ALGS[args.alg]
+    for tname, tid in (("rccl", 0), ("p2p", 1)):
+        if not headline.get(tname, {}).get("available", True) or S.lib().shmemx_set_transport(tid) < 0:
+            continue
+        rows = []
+        for m in sizes:
+            if m == args.n and "t_step" in headline.get(tname, {}):
+                ts = headline[tname]["t_step"]
+            else:
+                reps = max(3, min(args.steps, int(4e9 // (m * es))))
+                for _ in range(2):
+                    fn(team, dst, src, m)
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    fn(team, dst, src, m)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                el = torch.tensor([t1 - t0], dtype=torch.float64)
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                ts = el.item() / reps
+            wire = 2 * (P - 1) / P * m * es
+            row = {"nreduce": m, "ms_per_call": round(ts * 1e3, 4),
+                   "value_GiBs": round(world * m * es / ts / GiB, 3),
+                   "busbw_GBs": round(wire / ts / 1e9, 1),
+                   "frac_one_link": round(wire / ts / 1e9 / XGMI_LINK_GBS, 3),
+                   "frac_7_links": round(wire / ts / 1e9 / (XGMI_LINK_GBS * XGMI_LINKS), 3)}
+            if m == sizes[-1] and m != args.n:
+                cseed = seed + 211 + tid
+                L.fill(dt, dist_kind, cseed, rank, src, m, 0, stream)
+                torch.cuda.synchronize()
+                dist.barrier()
+                fn(team, dst, src, m)
+                mm = self_check(torch, L, S, dt, L.op_id(args.op), dist_kind, cseed, world, m, es,
+                                alg, dst, stream)
+                mmt = torch.tensor([mm], dtype=torch.int64)
+                dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
+                row["bitwise_mismatches_all_ranks"] = int(mmt.item())
+                L.fill(dt, dist_kind, seed, rank, src, args.n, 0, stream)
+                torch.cuda.synchronize()
+            rows.append(row)
+            log(f"[team curve] {tname} n={m} {row['ms_per_call']} ms/call {row['value_GiBs']} GiB/s "
+                f"busbw {row['busbw_GBs']} GB/s")
+        out[tname] = rows
+    S.lib().shmemx_set_transport(0)
+    return out
 
 
 def adjacent_collectives(args, torch, dist, L, S, dt, es, n, src, dst, stream, seed, rank, world):

@@ -94,7 +94,7 @@ def test_bench_team_leg(np_):
                         f"--nproc-per-node={np_}", "--master-addr", "127.0.0.1",
                         "--master-port", str(port), os.path.join(ROOT, "bench.py"),
                         "--gpus", str(np_), "--steps", "3", "--warmup", "1",
-                        "--nreduce", str((1 << 20) + 3)],
+                        "--nreduce", str((1 << 20) + 3), "--sweep-max", str(4 << 20)],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -106,3 +106,6 @@ def test_bench_team_leg(np_):
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0
     for coll in res.get("adjacent_collectives", {}).get("p2p", {}).values():
         assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]
+    curve = res["size_curve"]["p2p"]
+    assert [r["nreduce"] for r in curve] == [1 << 20, (1 << 20) + 3, 4 << 20]
+    assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
