@@ -122,6 +122,36 @@ __global__ __launch_bounds__(kThreads) void k_combine3_lds(T *out, const T *a,
     }
 }
 
+// Shape experiments (bench --variants): TPB threads per workgroup (tile = TPB 16-B
+// vectors per operand) and, with XCD = 1, an XCD-contiguous tile order: the dispatcher
+// deals consecutive workgroups round-robin to the 8 XCDs, so workgroup w runs on XCD
+// w % 8; tile = (w % 8) * per_xcd + w / 8 gives each XCD one contiguous stretch of the
+// vectors instead of every 8th tile.
+template <class T, class OP, int TPB, int XCD>
+__global__ __launch_bounds__(TPB) void k_combine3_x(T *out, const T *a, const T *b, Geom g,
+                                                   unsigned nvec_tiles)
+{
+    constexpr int V = Pack<T>::N;
+    const u32x4 *A = reinterpret_cast<const u32x4 *>(a + g.head);
+    const u32x4 *B = reinterpret_cast<const u32x4 *>(b + g.head);
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    const unsigned w = blockIdx.x;
+    if (w < nvec_tiles) {
+        size_t t = w;
+        if constexpr (XCD) {
+            const unsigned per = nvec_tiles / 8;   // host guarantees nvec_tiles % 8 == 0
+            t = (size_t)(w % 8) * per + w / 8;
+        }
+        const size_t i = t * TPB + threadIdx.x;
+        u32x4 ra = ldv<true>(A + i), rb = ldv<true>(B + i);
+        stv<true>(O + i, apply<T, OP>(ra, rb));
+    } else if (g.has_rem && threadIdx.x < kThreads) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
+        for (size_t i = g.head + (size_t)nvec_tiles * TPB * V + threadIdx.x; i < g.n; i += kThreads)
+            out[i] = OP::f(a[i], b[i]);
+    }
+}
+
 // Relative misalignment between the operands (not 16-B congruent): element loads.
 template <class T, class OP>
 __global__ __launch_bounds__(kThreads) void k_combine3_scalar(T *out, const T *a,
@@ -159,6 +189,11 @@ const VariantDesc kVariants[] = {
     {"buf_u4_sc1nt"},      // 12: aux sc1|nt both ways
     {"buf_u2_nt"},         // 13
     {"buf_u1_nt"},         // 14
+    {"x256_xcd"},          // 15: 256 threads, XCD-contiguous tiles
+    {"x512"},              // 16: 512 threads per workgroup (8 KiB tiles)
+    {"x1024"},             // 17: 1024 threads per workgroup
+    {"x512_xcd"},          // 18
+    {"x256"},              // 19: the k_combine3_x control (same shape as u1_nt)
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -169,6 +204,22 @@ int launch_combine3_vec(T *out, const T *a, const T *b, size_t n, hipStream_t st
     unsigned grid = grid_for(g, cap);
     hipLaunchKernelGGL((k_combine3<T, OP, U, NTL, NTS>), dim3(grid), dim3(kThreads), 0, st, out,
                        a, b, g);
+    return hip_ok(hipGetLastError());
+}
+
+template <class T, class OP, int TPB, int XCD>
+int launch_x(T *out, const T *a, const T *b, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), 1);
+    const size_t V = 16 / sizeof(T);
+    size_t tiles = (n - g.head) / V / TPB;
+    if (XCD) tiles -= tiles % 8;
+    g.tiles = tiles;
+    g.has_rem = (g.head > 0) || (tiles * TPB * V != n - g.head);
+    const unsigned grid = (unsigned)(tiles + (g.has_rem ? 1 : 0));
+    if (grid == 0) return SOSX_OK;
+    hipLaunchKernelGGL((k_combine3_x<T, OP, TPB, XCD>), dim3(grid), dim3(TPB), 0, st, out, a, b, g,
+                       (unsigned)tiles);
     return hip_ok(hipGetLastError());
 }
 
@@ -212,6 +263,11 @@ int launch_combine3(T *out, const T *a, const T *b, size_t n, hipStream_t st)
                 if (g_variant == 14) hipLaunchKernelGGL((k_combine3_buf<T, OP, 1, 2, 2>), gr, bl, 0, st, out, a, b, g);
                 return hip_ok(hipGetLastError());
             }
+            case 15: return launch_x<T, OP, 256, 1>(out, a, b, n, st);
+            case 16: return launch_x<T, OP, 512, 0>(out, a, b, n, st);
+            case 17: return launch_x<T, OP, 1024, 0>(out, a, b, n, st);
+            case 18: return launch_x<T, OP, 512, 1>(out, a, b, n, st);
+            case 19: return launch_x<T, OP, 256, 0>(out, a, b, n, st);
             default: break;
         }
     }

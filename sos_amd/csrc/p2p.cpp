@@ -23,6 +23,7 @@
 // For the SOS ring plan this is: fold chunk `me` straight from the P-1 peers' sources
 // over their xGMI links (P+1 HBM/xGMI streams, one launch), then gather the P-1 owned
 // chunks -- the RCCL version's scratch round trip disappears.
+#include <time.h>
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -72,16 +73,41 @@ P2PShared *shared()
     return (P2PShared *)st().shm.extra;
 }
 
+// Wall-clock bound of one wait (SHMEMX_P2P_TIMEOUT seconds, default 300): a peer that
+// never posts ends the job with a message instead of hanging it.
+double wait_limit_s()
+{
+    static const double lim = [] {
+        const char *e = getenv("SHMEMX_P2P_TIMEOUT");
+        const double v = e ? atof(e) : 0.0;
+        return v > 0 ? v : 300.0;
+    }();
+    return lim;
+}
+
+double now_s()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 void spin_until(std::atomic<uint64_t> &a, uint64_t want, const char *what)
 {
     unsigned spins = 0;
+    double t0 = 0;
     while (a.load(std::memory_order_acquire) < want) {
         if (++spins < 4096) {
             __builtin_ia32_pause();
             continue;
         }
         sched_yield();
-        if (spins > (1u << 30)) raise_error("p2p transport: timed out waiting for %s", what);
+        if ((spins & 1023) == 0) {
+            const double t = now_s();
+            if (t0 == 0) t0 = t;
+            else if (t - t0 > wait_limit_s())
+                raise_error("p2p transport: timed out after %.0f s waiting for %s", t - t0, what);
+        }
     }
 }
 

@@ -50,6 +50,7 @@ def main(args, torch):
     os.environ.setdefault("SHMEMX_DEVICE_HEAP_SIZE", str(2 * nmax * es + (320 << 20)))
     os.environ.setdefault("SHMEMX_STAGE_BYTES", str(64 << 20))
     os.environ.setdefault("SHMEMX_DEVICE", str(local))
+    os.environ.setdefault("SHMEMX_P2P_TIMEOUT", "120")
     dist.init_process_group("gloo")
     S.shmem_init()
     assert S.shmem_n_pes() == world and S.shmem_my_pe() == rank
