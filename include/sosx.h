@@ -160,6 +160,8 @@ int sosx_gather(int nseg, const void *const *srcs, void *const *dsts, const size
 int sosx_set_combine_variant(int variant);
 int sosx_num_combine_variants(void);
 const char *sosx_combine_variant_name(int variant);
+/* Same for the 8-input fp32 sum fold: 0 = default (U=1), 1 = U=2, 2 = U=4. */
+int sosx_set_fold_variant(int variant);
 
 /* Library / build identification. */
 const char *sosx_build_info(void);

@@ -227,6 +227,17 @@ using namespace sos;
 
 namespace {
 
+int g_fold_variant = 0;  // tuning experiments on the 8-input fp32 sum fold (bench A/B)
+
+template <class T, class OP, int NP, int ORDER, int U>
+int launch_fold_u(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), U);
+    hipLaunchKernelGGL((k_fold<T, OP, NP, ORDER, U>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
+                       0, st, out, ins, g);
+    return hip_ok(hipGetLastError());
+}
+
 template <class T, class OP, int NP, int ORDER>
 int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 {
@@ -239,6 +250,11 @@ int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
         hipLaunchKernelGGL((k_fold_scalar<T, OP, NP, ORDER>), dim3((unsigned)blocks),
                            dim3(kThreads), 0, st, out, ins, n);
         return hip_ok(hipGetLastError());
+    }
+    if constexpr (std::is_same<T, float>::value && std::is_same<OP, OpSum>::value && NP == 8 &&
+                  ORDER == SOSX_ORDER_LINEAR) {
+        if (g_fold_variant == 1) return launch_fold_u<T, OP, NP, ORDER, 2>(out, ins, n, st);
+        if (g_fold_variant == 2) return launch_fold_u<T, OP, NP, ORDER, 4>(out, ins, n, st);
     }
     constexpr int U = NP <= 2 ? 4 : (NP <= 4 ? 2 : 1);
     Geom g = make_geom(o, n, sizeof(T), U);
@@ -337,6 +353,15 @@ int sosx_prefix(int op, int dtype, void *const *outs, const void *const *ins, in
         pp.out[k] = outs[k];
     }
     return dispatch<PrefixFn>(op, dtype, &pp, np, own, count, as_stream(stream));
+}
+
+// Tuning knob (bench A/B only): 0 = default, 1 = U=2, 2 = U=4 for the 8-input fp32
+// sum LINEAR fold.  Returns the previous value.
+int sosx_set_fold_variant(int v)
+{
+    const int prev = g_fold_variant;
+    if (v >= 0 && v <= 2) g_fold_variant = v;
+    return prev;
 }
 
 int sosx_fold(int op, int dtype, int order, void *out, const void *const *ins, int nin,

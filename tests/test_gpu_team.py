@@ -187,3 +187,23 @@ def test_error_aborts_like_sos():
              "S.shmem_int_sum_reduce(S.team_world(), a.ctypes.data + 4, a.ctypes.data, 4)\n")
     r = _run(["python", "-c", code2], env={"PYTHONPATH": ROOT})
     assert r.returncode == 1 and "overlaps" in r.stderr
+
+
+def test_init_attr_one_pe():
+    """shmemx_get_unique_id + shmemx_init_attr (no TCP bootstrap, no node shared memory):
+    a reduction, a team split (agreement path without shm) and finalize."""
+    code = ("import numpy as np, ctypes\nfrom sos_amd import shmem as S\n"
+            "uid = S.get_unique_id()\nS.init_attr(0, 1, uid)\n"
+            "assert S.shmem_n_pes() == 1 and S.shmem_my_pe() == 0\n"
+            "a = np.arange(1000, dtype=np.int64); b = np.zeros_like(a)\n"
+            "assert S.shmem_int64_xor_reduce(S.team_world(), b.ctypes.data, a.ctypes.data, 1000) == 0\n"
+            "assert np.array_equal(a, b)\n"
+            "t = ctypes.c_void_p()\n"
+            "rc = S.lib().shmem_team_split_strided(ctypes.c_void_p(S.team_world()), 0, 1, 1, None, 0,"
+            " ctypes.byref(t))\n"
+            "assert rc == 0 and t.value, rc\n"
+            "S.lib().shmem_team_destroy(t)\n"
+            "S.lib().shmem_finalize()\nprint('init_attr ok')\n")
+    r = _run(["python", "-c", code], env={"PYTHONPATH": ROOT})
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "init_attr ok" in r.stdout

@@ -23,7 +23,12 @@ def main():
     ap.add_argument("--dtype", default="float")
     ap.add_argument("--op", default="sum")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--fold-ab", action="store_true",
+                    help="interleaved A/B of the fold variants (sosx_set_fold_variant) on P "
+                         "resident chunks of n/P elements")
     a = ap.parse_args()
+    if a.fold_ab:
+        return fold_ab(a)
     import torch
     from sos_amd import _lib as L
     from sos_amd import shmem as S
@@ -70,6 +75,43 @@ def main():
            "wall_ms_per_allreduce_all_PEs": round((t1 - t0) / a.iters * 1e3, 3),
            "mismatches_pe0": bad}
     print(json.dumps(out))
+
+
+def fold_ab(a, rounds=7, reps=20):
+    import torch
+    from sos_amd import _lib as L
+    torch.cuda.set_device(0)
+    dt, op = L.dtype_id(a.dtype), L.op_id(a.op)
+    es = L.dtype_size(dt)
+    chunk = a.n // a.P
+    ins = [torch.empty(chunk * es, dtype=torch.uint8, device="cuda") for _ in range(a.P)]
+    for k, b in enumerate(ins):
+        L.fill(dt, 0, 0x5EED, k, b.data_ptr(), chunk)
+    outs = {v: torch.empty_like(ins[0]) for v in range(3)}
+    lib = L.lib()
+    ptrs = [b.data_ptr() for b in ins]
+    res = {v: [] for v in range(3)}
+    for _ in range(rounds):
+        for v in range(3):
+            lib.sosx_set_fold_variant(v)
+            for _ in range(3):
+                L.fold(op, dt, L.ORDER_LINEAR, outs[v].data_ptr(), ptrs, chunk)
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            for _ in range(reps):
+                L.fold(op, dt, L.ORDER_LINEAR, outs[v].data_ptr(), ptrs, chunk)
+            s1.record()
+            torch.cuda.synchronize()
+            res[v].append(s0.elapsed_time(s1) / reps)
+    lib.sosx_set_fold_variant(0)
+    same = all(torch.equal(outs[0], outs[v]) for v in (1, 2))
+    algo = (a.P + 1) * chunk * es
+    rows = {}
+    for v, name in ((0, "u1"), (1, "u2"), (2, "u4")):
+        ms = sorted(res[v])[len(res[v]) // 2]
+        rows[name] = {"median_ms": round(ms, 5), "GBs": round(algo / (ms / 1e3) / 1e9, 1)}
+    print(json.dumps({"fold_ab": rows, "P": a.P, "chunk": chunk, "bytes": algo,
+                      "variants_bit_identical": same}))
 
 
 if __name__ == "__main__":
