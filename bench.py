@@ -115,19 +115,31 @@ def run_combine(args, torch):
     for _ in range(args.warmup):
         launch()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # Timed region: the K launches back to back on the library's stream, bracketed by two
+    # HIP events (and the host clock).  Per-launch event pairs would add two queue
+    # packets to every step; the span / K is the per-launch duration INCLUDING the
+    # dependent-launch boundary, so `achieved` is conservative against rocprof's
+    # kernel-only average.
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+    e0.record(stream)
+    for _ in range(args.steps):
         launch()
-        e.record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    kern_ms = sorted(s.elapsed_time(e) for s, e in ev)
-    mean_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+    mean_kern_s = e0.elapsed_time(e1) / args.steps / 1e3
     step_s = (t1 - t0) / args.steps
+    # per-launch event pairs, after the timed region: the kernel-only median
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(min(args.steps, 20))]
+    for s_, e_ in ev:
+        s_.record(stream)
+        launch()
+        e_.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = sorted(s_.elapsed_time(e_) for s_, e_ in ev)
     payload = args.n * es
     algo_bytes = 3 * payload  # read in, read inout, write inout
     achieved = algo_bytes / mean_kern_s / 1e9
@@ -153,7 +165,9 @@ def run_combine(args, torch):
                      "traffic": None,
                      "kernel": "sos::k_combine3", "algorithmic_bytes_per_launch": algo_bytes,
                      "mean_kernel_ms": round(mean_kern_s * 1e3, 5),
-                     "median_kernel_ms": round(kern_ms[len(kern_ms) // 2], 5)},
+                     "mean_kernel_ms_how": "HIP-event span of the timed region / steps",
+                     "median_kernel_ms": round(kern_ms[len(kern_ms) // 2], 5),
+                     "median_kernel_ms_how": "per-launch HIP event pairs, after the timed region"},
     }
     return res
 
