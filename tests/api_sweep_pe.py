@@ -100,6 +100,7 @@ def main():
                 nd = int(np.count_nonzero(np.frombuffer(got.tobytes(), np.uint8)
                                           != np.frombuffer(ref.tobytes(), np.uint8)))
                 bad.append((name, n, f"{nd} bytes differ"))
+    checks += sweep_scans_bcasts(world, me, P, bad)
     S.shmem_barrier_all()
     S.shmem_finalize()
     if bad:
@@ -107,6 +108,70 @@ def main():
         return 1
     print(f"PE {me}/{P}: {checks} checks OK", flush=True)
     return 0
+
+
+CSIZE = {"float": 4, "double": 8, "long double": 16, "char": 1, "signed char": 1, "short": 2,
+         "int": 4, "long": 8, "long long": 8, "unsigned char": 1, "unsigned short": 2,
+         "unsigned int": 4, "unsigned long": 8, "unsigned long long": 8, "int8_t": 1,
+         "int16_t": 2, "int32_t": 4, "int64_t": 8, "uint8_t": 1, "uint16_t": 2, "uint32_t": 4,
+         "uint64_t": 8, "size_t": 8, "ptrdiff_t": 8}
+
+
+def _buffers(src, n_bytes_on_device):
+    """(src_ptr, dst_ptr, read_dst) for host (small) or device (large) operands."""
+    if not n_bytes_on_device:
+        dst = np.full(src.nbytes, 0x5A, np.uint8)
+        return src.ctypes.data, dst.ctypes.data, lambda: dst.tobytes(), (src, dst)
+    t_src = torch.from_numpy(np.frombuffer(src.tobytes(), np.uint8).copy()).cuda()
+    t_dst = torch.full_like(t_src, 0x5A)
+    torch.cuda.synchronize()
+    return t_src.data_ptr(), t_dst.data_ptr(), lambda: t_dst.cpu().numpy().tobytes(), (t_src, t_dst)
+
+
+def sweep_scans_bcasts(world, me, P, bad):
+    """The 52 team scans shmemx_<T>_sum_{inscan,exscan} (oracle.scan = SOS scan_ring,
+    src/collectives.c:1111-1209) and the 24 typed team broadcasts shmem_<T>_broadcast
+    from team PE 1 % P (oracle.bcast, src/collectives.c:429-485)."""
+    checks = 0
+    for (st, ct, it), kind in G.SCANS:
+        dt = L.dtype_id(ITYPE[it])
+        name = f"shmemx_{st}_sum_{kind}"
+        fn = getattr(S.lib(), name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        for n in (37, 5000):
+            seed = zlib.crc32(f"{name}/{n}".encode())
+            ins = [make_input(dt, 0, seed, pe, n) for pe in range(P)]
+            ref = O.scan(5, dt, ins, kind == "exscan",
+                         [np.frombuffer(np.full(ins[0].nbytes, 0x5A, np.uint8).tobytes(),
+                                        ins[0].dtype).copy() for _ in range(P)])[me]
+            sp, dp, read, keep = _buffers(ins[me], n == 5000)
+            rc = fn(world, dp, sp, n)
+            checks += 1
+            if rc != 0 or read() != ref.tobytes():
+                bad.append((name, n, "rc" if rc else "bytes differ"))
+            del keep
+    root = 1 % P
+    for st, ct in G.RMA:
+        es = CSIZE[ct]
+        name = f"shmem_{st}_broadcast"
+        fn = getattr(S.lib(), name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                       ctypes.c_int]
+        for n in (37, 5000):
+            seed = zlib.crc32(f"{name}/{n}".encode())
+            srcs = [np.random.default_rng(seed * 64 + pe).integers(0, 256, n * es, dtype=np.uint8)
+                    for pe in range(P)]
+            init = [np.full(n * es, 0x5A, np.uint8) for _ in range(P)]
+            ref = O.bcast(srcs, root, True, init)[me]
+            sp, dp, read, keep = _buffers(srcs[me], n == 5000)
+            rc = fn(world, dp, sp, n, root)
+            checks += 1
+            if rc != 0 or read() != ref.tobytes():
+                bad.append((name, n, "rc" if rc else "bytes differ"))
+            del keep
+    return checks
 
 
 if __name__ == "__main__":

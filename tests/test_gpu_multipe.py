@@ -113,10 +113,11 @@ def test_bench_team_leg(np_):
 
 @pytest.mark.parametrize("np_", [3, 4])
 def test_api_sweep_every_typed_reduction(np_):
-    """All 198 typed reductions (154 *_reduce + 44 *_to_all) across np_ real PE processes,
-    host and device buffers, recdbl and ring sizes, bit for bit vs the oracle schedules."""
+    """All 198 typed reductions (154 *_reduce + 44 *_to_all), the 52 typed scans and the 24
+    typed broadcasts across np_ real PE processes, host and device buffers, recdbl and
+    ring sizes, bit for bit vs the oracle schedules."""
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "api_sweep_pe.py")], timeout=600)
     ok = re.findall(r"PE (\d+)/\d+: (\d+) checks OK", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
         r.stdout[-3000:] + r.stderr[-3000:]
-    assert all(int(c) == 396 for _, c in ok), ok
+    assert all(int(c) == 396 + 104 + 48 for _, c in ok), ok
