@@ -319,7 +319,7 @@ void sos_api_to_all(void *target, const void *source, int nreduce, size_t type_s
     check_initialized(fn);
     State &s = st();
     const int stride = 1 << logPE_stride;
-    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) > s.n_pes)
+    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) >= s.n_pes)
         raise_error("%s: Invalid active set (PE_start = %d, PE_stride = %d, PE_size = %d)", fn,
                     PE_start, stride, PE_size);
     if (!(s.my_pe >= PE_start && s.my_pe <= PE_start + ((PE_size - 1) * stride) &&
@@ -395,7 +395,7 @@ static void bcast_active_set(void *target, const void *source, size_t nlong, siz
     check_initialized(fn);
     State &s = st();
     const int stride = 1 << logPE_stride;
-    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) > s.n_pes)
+    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) >= s.n_pes)
         raise_error("%s: Invalid active set (PE_start = %d, PE_stride = %d, PE_size = %d)", fn,
                     PE_start, stride, PE_size);
     if (!(s.my_pe >= PE_start && s.my_pe <= PE_start + ((PE_size - 1) * stride) &&

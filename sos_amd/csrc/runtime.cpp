@@ -770,8 +770,10 @@ static Team active_set(int PE_start, int logPE_stride, int PE_size, const char *
 {
     State &s = st();
     const int stride = 1 << logPE_stride;
-    // SHMEM_ERR_CHECK_ACTIVE_SET (src/shmem_internal.h:214-227)
-    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) > s.n_pes)
+    // SHMEM_ERR_CHECK_ACTIVE_SET (src/shmem_internal.h:214-227).  SOS tests the last PE
+    // with `> num_pes`, which admits PE num_pes (no such PE: SOS then waits on it forever);
+    // here that set is refused, since a transfer to it would index past the PE tables.
+    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) >= s.n_pes)
         raise_error("%s: Invalid active set (PE_start = %d, PE_stride = %d, PE_size = %d)", fn,
                     PE_start, stride, PE_size);
     if (!(s.my_pe >= PE_start && s.my_pe <= PE_start + ((PE_size - 1) * stride) &&

@@ -182,6 +182,10 @@ def test_error_aborts_like_sos():
     r = _run(["python", "-c", code], env={"PYTHONPATH": ROOT})
     assert r.returncode == 1
     assert "Invalid active set" in r.stderr
+    # the set {0, 1} on a 1-PE job: SOS's `> num_pes` test admits it (and then waits on the
+    # missing PE 1); this build refuses it
+    r = _run(["python", "-c", code.replace("4, 0, 0, 5,", "4, 0, 0, 2,")], env={"PYTHONPATH": ROOT})
+    assert r.returncode == 1 and "Invalid active set" in r.stderr, r.stderr[-2000:]
     code2 = ("import numpy as np\nfrom sos_amd import shmem as S\nS.shmem_init()\n"
              "a = np.zeros(8, np.int32)\n"
              "S.shmem_int_sum_reduce(S.team_world(), a.ctypes.data + 4, a.ctypes.data, 4)\n")
