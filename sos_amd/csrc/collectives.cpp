@@ -188,6 +188,36 @@ const char *status_text(int rc)
     }
 }
 
+// The peer-to-peer leg of execute(): operands in the IPC-mapped heap run in place,
+// others are staged through the stage region; scan scratch follows the staged operand.
+void execute_p2p(const Plan &p, const Team &t, int alg, size_t count, size_t ts, const void *source,
+                 void *target, const char *dsrc, char *ddst, bool direct, size_t base, int op,
+                 int dt, const char *fn)
+{
+    State &s = st();
+    const size_t bytes = count * ts;
+    const char *hb = s.sym_stage;
+    if (!direct && p.reads_src)
+        hip_check(hipMemcpyAsync(s.sym_stage, source, bytes, hipMemcpyDefault, s.stream), "stage in");
+    char *scr = nullptr;
+    size_t scr_off = 0;
+    if (p.scratch_bytes && p.scr_sent) {
+        scr = s.sym_stage + base;
+        scr_off = base;
+    } else if (p.scratch_bytes) {
+        scr = (char *)scratch(p.scratch_bytes);
+    }
+    const unsigned smis = (unsigned)((uintptr_t)dsrc & 15), dmis = (unsigned)((uintptr_t)ddst & 15);
+    P2PBufs pb{dsrc, ddst, scr, (size_t)(dsrc - hb), (size_t)(ddst - hb), scr_off, smis, dmis};
+    if (g_prof.on) g_prof.ncall++;
+    int rc = p2p_exec(p, t, alg, count, ts, pb, op, dt, s.stream);
+    if (rc) raise_error("%s: %s", fn, status_text(rc));
+    if (!direct && p.writes_dst)
+        hip_check(hipMemcpyAsync(target, s.sym_stage, bytes, hipMemcpyDefault, s.stream), "stage out");
+    hip_check(hipStreamSynchronize(s.stream), fn);
+    if (g_prof.on) g_prof.collect();
+}
+
 // Run plan `alg` (a reduction SOSX_ALG_*, a scan or a broadcast, plan.h) for this PE
 // over team t, on the library stream; returns when the call is complete.
 void execute(int alg, void *target, const void *source, size_t count, size_t ts, const Team &t,
@@ -204,43 +234,26 @@ void execute(int alg, void *target, const void *source, size_t count, size_t ts,
             return hb && (const char *)p >= hb && (const char *)p + bytes <= hb + s.dev_heap_bytes;
         };
         const bool direct = in_heap(source) && in_heap(target);
-        const char *dsrc = (const char *)source;
-        char *ddst = (char *)target;
-        if (!direct) {
-            if (bytes > s.sym_stage_bytes)
-                raise_error("%s: %zu bytes outside the device symmetric heap exceed the p2p stage "
-                            "region (SHMEMX_STAGE_BYTES=%zu); allocate with shmemx_malloc_device",
-                            fn, bytes, s.sym_stage_bytes);
-            dsrc = ddst = s.sym_stage;
-        }
+        const char *dsrc = direct ? (const char *)source : s.sym_stage;
+        char *ddst = direct ? (char *)target : s.sym_stage;
         const unsigned smis = (unsigned)((uintptr_t)dsrc & 15), dmis = (unsigned)((uintptr_t)ddst & 15);
         const Plan &p = cached_plan(alg, t.size, t.my_idx, count, ts, smis, dmis);
-        if (!direct && p.reads_src)
-            hip_check(hipMemcpyAsync(s.sym_stage, source, bytes, hipMemcpyDefault, s.stream), "stage in");
-        // scratch the peers read (scan results) lives in the stage region, after any
-        // staged operand; private scratch in the library's device buffer
-        char *scr = nullptr;
-        size_t scr_off = 0;
-        if (p.scratch_bytes && p.scr_sent) {
-            const size_t base = direct ? 0 : (bytes + 255) / 256 * 256;
-            if (base + p.scratch_bytes > s.sym_stage_bytes)
-                raise_error("%s: %zu bytes of exchange scratch exceed the p2p stage region "
-                            "(SHMEMX_STAGE_BYTES=%zu)", fn, (size_t)(base + p.scratch_bytes),
-                            s.sym_stage_bytes);
-            scr = s.sym_stage + base;
-            scr_off = base;
-        } else if (p.scratch_bytes) {
-            scr = (char *)scratch(p.scratch_bytes);
+        // the staged operand and the scratch the peers read (scan results) must fit the
+        // IPC-mapped stage region; the decision depends only on sizes, residency of
+        // symmetric addresses and SHMEMX_STAGE_BYTES, so every PE takes the same branch
+        const size_t base = direct ? 0 : (bytes + 255) / 256 * 256;
+        const size_t need = (p.scratch_bytes && p.scr_sent) ? base + p.scratch_bytes : (direct ? 0 : bytes);
+        if (need <= s.sym_stage_bytes) {
+            execute_p2p(p, t, alg, count, ts, source, target, dsrc, ddst, direct, base, op, dt, fn);
+            return;
         }
-        P2PBufs pb{dsrc, ddst, scr, (size_t)(dsrc - hb), (size_t)(ddst - hb), scr_off, smis, dmis};
-        if (g_prof.on) g_prof.ncall++;
-        rc = p2p_exec(p, t, alg, count, ts, pb, op, dt, s.stream);
-        if (rc) raise_error("%s: %s", fn, status_text(rc));
-        if (!direct && p.writes_dst)
-            hip_check(hipMemcpyAsync(target, s.sym_stage, bytes, hipMemcpyDefault, s.stream), "stage out");
-        hip_check(hipStreamSynchronize(s.stream), fn);
-        if (g_prof.on) g_prof.collect();
-        return;
+        if (!s.comm)
+            raise_error("%s: %zu bytes (staged operand + exchange scratch) exceed the p2p stage "
+                        "region (SHMEMX_STAGE_BYTES=%zu); allocate operands with "
+                        "shmemx_malloc_device or raise SHMEMX_STAGE_BYTES", fn, need,
+                        s.sym_stage_bytes);
+        // both transports are up: this call runs on RCCL instead
+        debug_msg("%s: %zu bytes exceed the p2p stage region, call runs on RCCL", fn, need);
     }
 
     // residency: device pointers run in place; host memory is staged through HBM

@@ -235,13 +235,29 @@ void ensure_device_heap()
     State &s = st();
     if (s.dev_heap.base) return;
     char *base = nullptr;
+    // HIP runtimes before 7.2 (torch 2.10's bundled 7.0.2 among them) hang in
+    // hipIpcOpenMemHandle when the exported allocation's size has bit 31 set (2-4 GiB,
+    // 6-8 GiB, ...: measured with tests/heap_init_pe.py and tools/diag/heap_probe.c); 7.2 maps every size.  An
+    // exported heap is therefore rounded up past such sizes on those runtimes.
+    const bool exported = s.want_p2p && s.n_pes > 1;
+    int rtv = 0;
+    (void)hipRuntimeGetVersion(&rtv);
+    const bool ipc_size_bug = rtv < 70200000;
     if (s.ext_base) {
         base = (char *)s.ext_base;
         s.dev_heap_bytes = s.ext_size;
         if (s.sym_stage_bytes >= s.ext_size) s.sym_stage_bytes = s.ext_size / 2;
     } else {
+        if (exported && ipc_size_bug && (s.dev_heap_bytes & 0x80000000ull)) {
+            const size_t want = s.dev_heap_bytes;
+            s.dev_heap_bytes = (s.dev_heap_bytes | 0xFFFFFFFFull) + 1;
+            debug_msg("device heap %zu B rounded up to %zu B (HIP %d IPC size limitation)", want,
+                      s.dev_heap_bytes, rtv);
+        }
         hip_check(hipMalloc((void **)&base, s.dev_heap_bytes), "hipMalloc(device heap)");
     }
+    debug_msg("device heap %zu B at %p (stage %zu B)", s.dev_heap_bytes, (void *)base,
+              s.sym_stage_bytes);
     s.sym_stage = base;
     s.dev_heap.init(base + s.sym_stage_bytes, s.dev_heap_bytes - s.sym_stage_bytes, true,
                     s.ext_base != nullptr);
@@ -253,10 +269,21 @@ void ensure_device_heap()
     // p2p-only mode cannot run without the mapping; in `both` mode a failure on any PE
     // turns the p2p transport off on every PE (agreed through the hub)
     const bool fatal = s.transport == TRANSPORT_P2P;
+    if (s.ext_base && ipc_size_bug && (s.dev_heap_bytes & 0x80000000ull)) {
+        // an external heap of such a size cannot be mapped on this runtime
+        if (fatal)
+            raise_error("shmemx_heap_create: a %zu-byte external heap cannot be IPC-mapped by HIP "
+                        "runtime %d (sizes with bit 31 set hang before 7.2); use another size",
+                        s.dev_heap_bytes, rtv);
+        warn("external heap of %zu B cannot be IPC-mapped by HIP %d: p2p transport off",
+             s.dev_heap_bytes, rtv);
+        return;
+    }
     hipIpcMemHandle_t mine;
     memset(&mine, 0, sizeof(mine));
     hipError_t e = hipIpcGetMemHandle(&mine, base);
     if (e != hipSuccess && fatal) hip_check(e, "hipIpcGetMemHandle(device heap)");
+    debug_msg("device heap: IPC handle %s", e == hipSuccess ? "ok" : hipGetErrorString(e));
     std::vector<hipIpcMemHandle_t> all((size_t)s.n_pes);
     if (sosboot::hub_allgather(&s.hub, &mine, sizeof(mine), all.data()) != 0)
         raise_error("device heap: IPC handle exchange failed");
@@ -264,7 +291,9 @@ void ensure_device_heap()
     for (int q = 0; q < s.n_pes && ok; ++q) {
         if (q == s.my_pe) continue;
         void *p = nullptr;
+        debug_msg("device heap: opening PE %d's handle", q);
         hipError_t eo = hipIpcOpenMemHandle(&p, all[(size_t)q], hipIpcMemLazyEnablePeerAccess);
+        debug_msg("device heap: PE %d mapped at %p (%s)", q, p, hipGetErrorString(eo));
         if (eo != hipSuccess) {
             if (fatal) hip_check(eo, "hipIpcOpenMemHandle(peer device heap)");
             (void)hipGetLastError();

@@ -15,10 +15,13 @@ re-evaluates the schedule's element order with the fold kernel (ring: chunk c fo
 from PE c rightwards, src/collectives.c:693-727; tree schedules: the recdbl_sw tree),
 then compares its team result bit for bit.
 """
+import ctypes
 import json
 import os
 import sys
 import time
+
+ctypes_u8 = ctypes.c_uint8
 
 GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0
@@ -47,10 +50,14 @@ def main(args, torch):
         [m for m in (1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20)
          if m != n and m <= getattr(args, "sweep_max", 256 << 20)]
     nmax = max([n] + sweep_sizes)
-    os.environ.setdefault("SHMEMX_DEVICE_HEAP_SIZE", str(2 * nmax * es + (320 << 20)))
-    os.environ.setdefault("SHMEMX_STAGE_BYTES", str(64 << 20))
+    # p2p stage region: the scans' exchange scratch (2(P-1)/P * n * s) and staged host
+    # operands must fit it, or those calls run on RCCL instead
+    stage = 2 * n * es + (64 << 20)
+    os.environ.setdefault("SHMEMX_STAGE_BYTES", str(stage))
+    os.environ.setdefault("SHMEMX_DEVICE_HEAP_SIZE", str(2 * nmax * es + stage + (320 << 20)))
     os.environ.setdefault("SHMEMX_DEVICE", str(local))
     os.environ.setdefault("SHMEMX_P2P_TIMEOUT", "120")
+    os.environ.setdefault("SHMEM_SYMMETRIC_SIZE", str(2 * (16 << 20) * es + (64 << 20)))
     dist.init_process_group("gloo")
     S.shmem_init()
     assert S.shmem_n_pes() == world and S.shmem_my_pe() == rank
@@ -74,10 +81,14 @@ def main(args, torch):
         fn(team, dst, src, n)
 
     results = {}
+    if rank == 0:
+        log(f"[team] {world} PEs, nreduce {n}, alg {name}: heap {os.environ['SHMEMX_DEVICE_HEAP_SIZE']} B")
     for tname, tid in (("rccl", 0), ("p2p", 1)):
         if S.lib().shmemx_set_transport(tid) < 0:
             results[tname] = {"available": False}
             continue
+        if rank == 0:
+            log(f"[team] {tname}: warmup + {args.steps} timed steps")
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
@@ -115,6 +126,10 @@ def main(args, torch):
 
     curve = size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
                        src, dst, stream, sorted(sweep_sizes + [n]), results) if sweep_sizes else {}
+
+    host_leg = {} if getattr(args, "no_host", False) else \
+        host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank,
+                           world, stream, results)
 
     adjacent = {}
     if not getattr(args, "no_adjacent", False):
@@ -181,6 +196,8 @@ def main(args, torch):
                                "(SHMEMX_TRANSPORT selects)")
     if curve:
         res["size_curve"] = curve
+    if host_leg:
+        res["host_resident"] = host_leg
     if adjacent:
         res["adjacent_collectives"] = adjacent
     if rank == 0:
@@ -191,6 +208,49 @@ def main(args, torch):
     S.shmem_finalize()
     dist.destroy_process_group()
     return 0
+
+
+def host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
+                       stream, headline):
+    """The same team reduction when source/dest live in the HOST symmetric heap (SOS's
+    own case: shmem_malloc returns pinned host memory here): H2D staging, the device team
+    reduction, D2H -- the PCIe-inclusive rate the north star asks to record beside
+    `value`.  nreduce = min(n, 16Mi) (64 MiB fp32: the p2p stage region's size)."""
+    import numpy as np
+    m = min(args.n, 16 << 20)
+    nbytes = m * es
+    hsrc = S.lib().shmem_malloc(nbytes)
+    hdst = S.lib().shmem_malloc(nbytes)
+    if not hsrc or not hdst:
+        return {"skipped": "shmem_malloc failed (SHMEM_SYMMETRIC_SIZE)"}
+    tmp = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    L.fill(dt, dist_kind, seed, rank, tmp.data_ptr(), m, 0, stream)
+    torch.cuda.synchronize()
+    host = np.ctypeslib.as_array((ctypes_u8 * nbytes).from_address(hsrc))
+    host[:] = tmp.cpu().numpy()
+    out = {"nreduce": m, "buffers": "shmem_malloc (pinned host symmetric heap)"}
+    for tname, tid in (("rccl", 0), ("p2p", 1)):
+        if not headline.get(tname, {}).get("available", True) or S.lib().shmemx_set_transport(tid) < 0:
+            continue
+        reps = max(3, min(args.steps, 10))
+        fn(team, hdst, hsrc, m)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn(team, hdst, hsrc, m)
+        t1 = time.perf_counter()
+        el = torch.tensor([t1 - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        ts = el.item() / reps
+        out[tname] = {"ms_per_call": round(ts * 1e3, 4),
+                      "value_GiBs": round(world * nbytes / ts / GiB, 3),
+                      "payload_GiBs_per_pe": round(nbytes / ts / GiB, 3),
+                      "pcie_bytes_per_pe": 2 * nbytes}
+        log(f"[host resident] {tname} n={m} {out[tname]['ms_per_call']} ms/call")
+    S.lib().shmemx_set_transport(0)
+    S.lib().shmem_free(hdst)
+    S.lib().shmem_free(hsrc)
+    return out
 
 
 def size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world, src, dst,

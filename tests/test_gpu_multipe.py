@@ -106,6 +106,7 @@ def test_bench_team_leg(np_):
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0
     for coll in res.get("adjacent_collectives", {}).get("p2p", {}).values():
         assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]
+    assert res["host_resident"]["p2p"]["value_GiBs"] > 0, res["host_resident"]
     curve = res["size_curve"]["p2p"]
     assert [r["nreduce"] for r in curve] == [1 << 20, (1 << 20) + 3, 4 << 20]
     assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
@@ -121,3 +122,40 @@ def test_api_sweep_every_typed_reduction(np_):
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
         r.stdout[-3000:] + r.stderr[-3000:]
     assert all(int(c) == 396 + 104 + 48 for _, c in ok), ok
+
+
+def test_p2p_stage_overflow_is_an_error(tmp_path):
+    """p2p-only transport: a scan whose exchange scratch exceeds SHMEMX_STAGE_BYTES ends the
+    job with a message (with RCCL also up -- SHMEMX_TRANSPORT=both -- the call runs on RCCL
+    instead; that needs one GPU per PE)."""
+    script = tmp_path / "ovf.py"
+    script.write_text(
+        "import torch\nfrom sos_amd import shmem as S\nS.shmem_init()\n"
+        "n = 1 << 20\nsrc = S.shmemx_malloc_device(n * 4)\ndst = S.shmemx_malloc_device(n * 4)\n"
+        "S.shmemx_float_sum_inscan(S.team_world(), dst, src, n)\nprint('no error')\n")
+    env_stage = dict(os.environ, SHMEMX_STAGE_BYTES="1M")
+    env = dict(env_stage)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update({"SHMEMX_TRANSPORT": "p2p", "SHMEMX_DEVICE_HEAP_SIZE": "64M", "SHMEMX_DEVICE": "0",
+                "PYTHONPATH": ROOT})
+    r = subprocess.run([sys.executable, OSHRUN, "-np", "2", "--timeout", "100", sys.executable,
+                        str(script)], capture_output=True, text=True, timeout=150, env=env)
+    assert r.returncode != 0 and "no error" not in r.stdout
+    assert "exceed the p2p stage region" in r.stderr, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("heap", ["2G", "3400M"])
+def test_ipc_heap_sizes_with_bit31(heap):
+    """torch's HIP 7.0.2 hangs in hipIpcOpenMemHandle for exported sizes with bit 31 set;
+    the library rounds such heaps up (tests/heap_init_pe.py, tools/diag/heap_probe.c on /opt/rocm 7.2 maps them all)."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update({"SHMEMX_TRANSPORT": "p2p", "SHMEMX_DEVICE_HEAP_SIZE": heap, "SHMEMX_DEVICE": "0",
+                "SHMEMX_STAGE_BYTES": "64M", "PYTHONPATH": ROOT})
+    r = subprocess.run([sys.executable, OSHRUN, "-np", "2", "--timeout", "60", sys.executable,
+                        os.path.join(ROOT, "tests", "heap_init_pe.py")],
+                       capture_output=True, text=True, timeout=90, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert r.stdout.count("PE done") == 2, r.stdout
