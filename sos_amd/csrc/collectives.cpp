@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <algorithm>
 #include <deque>
 #include <map>
 #include <tuple>
@@ -218,6 +219,141 @@ void execute_p2p(const Plan &p, const Team &t, int alg, size_t count, size_t ts,
     if (g_prof.on) g_prof.collect();
 }
 
+// Host-resident ring reductions, pipelined in stripes.
+//
+// SOS's operands live in the host symmetric heap.  Staged whole, a call costs
+// H2D(n*s) + exchange + D2H(n*s) in sequence.  The ring's element order depends only on
+// which ring chunk an element is in (chunk c is folded starting at PE c,
+// src/collectives.c:693-727), so the vector is cut into stripes that take the k-th
+// slice of EVERY ring chunk: stripe k = concat over c of chunk c's elements
+// [k*L, k*L + L_k).  Run as an ordinary ring over its P*L_k elements, the stripe's chunk c
+// is exactly that slice of the full chunk c, owned and folded by PE c in the same order,
+// so the result is bit-identical to the ring over the whole vector (tests/test_stripes.py
+// checks this with the oracle).  The r = n mod P last elements of chunks c < r form a
+// final stripe of r elements (one per chunk: again the ring's own split).  Stripes flow
+// through three device slots:
+//   H2D(k+2) on a copy stream || exchange(k) on the library stream || D2H(k-1),
+// so a call approaches max(H2D, D2H) on a full-duplex PCIe link instead of their sum.
+// Returns false (nothing done) when the call does not qualify.
+bool striped_host_ring(int alg, void *target, const void *source, size_t count, size_t ts,
+                       const Team &t, int op, int dt, const char *fn)
+{
+    State &s = st();
+    const int P = t.size;
+    if (alg != SOSX_ALG_RING || P < 2 || P > SOSX_MAX_FOLD || s.host_stripe_bytes == 0) return false;
+    if (is_device_ptr(source) || is_device_ptr(target)) return false;
+    const size_t q = count / (size_t)P, r = count % (size_t)P;
+    // Stripe shape, from measurements of this stream/event pattern on MI355X with HIP 7.0
+    // (tools/diag/stripe_probe.py): pinned copies under ~4 MiB, or more than ~16 stripes
+    // in flight, make the runtime serialise the three streams (a 512 MiB pass at 32
+    // stripes took 2x the serial time); at <= 8 stripes of >= 4 MiB pieces a pass took
+    // 0.67x.  So: pieces of >= SHMEMX_HOST_STRIPE_BYTES (default 4 MiB), at most 8
+    // stripes.  The p2p executor synchronises the host every round, which leaves the copy
+    // streams little to overlap: it stripes only when SHMEMX_HOST_STRIPE_BYTES is set
+    // explicitly (the tests use tiny stripes to exercise the decomposition).
+    const bool p2p = s.transport == TRANSPORT_P2P;
+    if (p2p && !s.host_stripe_explicit) return false;
+    size_t L = (s.host_stripe_bytes + ts - 1) / ts;
+    if (!s.host_stripe_explicit) L = std::max(L, (q + 7) / 8);
+    if (p2p) {  // three slots in the IPC-mapped stage region
+        const size_t lim = s.sym_stage_bytes / 3 / ((size_t)P * ts);
+        if (lim < L) L = lim;
+    }
+    if (L == 0 || q < 2 * L) return false;
+    const size_t slot_bytes = ((size_t)P * L * ts + 255) / 256 * 256;
+    char *slots;
+    if (p2p) {
+        slots = s.sym_stage;
+    } else {
+        if (s.stripes_bytes < 3 * slot_bytes) {
+            if (s.stripes) {
+                hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize");
+                hip_check(hipFree(s.stripes), "hipFree(stripes)");
+                s.stripes = nullptr;
+            }
+            hip_check(hipMalloc(&s.stripes, 3 * slot_bytes), "hipMalloc(stripes)");
+            s.stripes_bytes = 3 * slot_bytes;
+        }
+        slots = (char *)s.stripes;
+    }
+    if (!s.pipe_h2d) {
+        hip_check(hipStreamCreateWithFlags(&s.pipe_h2d, hipStreamNonBlocking), "hipStreamCreate");
+        hip_check(hipStreamCreateWithFlags(&s.pipe_d2h, hipStreamNonBlocking), "hipStreamCreate");
+        for (auto &slot : s.pipe_ev)
+            for (hipEvent_t &e : slot)
+                hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    }
+    enum { H2D = 0, XCH = 1, D2H = 2 };
+    const size_t nfull = (q + L - 1) / L;
+    const size_t nstripes = nfull + (r ? 1 : 0);
+    debug_msg("%s: host-resident ring in %zu stripes of %zu x %zu elements", fn, nstripes,
+              (size_t)P, L);
+    auto disp = [&](size_t c) { return c * q + (c < r ? c : r); };
+    // stripe k: slice length per chunk, first element of the slice within each chunk,
+    // and the number of chunks it takes a slice of
+    auto geom = [&](size_t k, size_t *len, size_t *first, size_t *npieces) {
+        if (k < nfull) {
+            *first = k * L;
+            *len = q - k * L < L ? q - k * L : L;
+            *npieces = (size_t)P;
+        } else {
+            *first = q;
+            *len = 1;
+            *npieces = r;
+        }
+    };
+    const char *src = (const char *)source;
+    char *dst = (char *)target;
+    auto h2d = [&](size_t k) {
+        const int sl = (int)(k % 3);
+        size_t len, first, np;
+        geom(k, &len, &first, &np);
+        char *slot = slots + (size_t)sl * slot_bytes;
+        hip_check(hipStreamWaitEvent(s.pipe_h2d, s.pipe_ev[sl][D2H], 0), "stripe wait");
+        for (size_t c = 0; c < np; ++c)
+            hip_check(hipMemcpyAsync(slot + c * len * ts, src + (disp(c) + first) * ts, len * ts,
+                                     hipMemcpyHostToDevice, s.pipe_h2d), "stripe H2D");
+        hip_check(hipEventRecord(s.pipe_ev[sl][H2D], s.pipe_h2d), "stripe event");
+    };
+    // every slot starts free: its "D2H done" event is recorded on the idle copy stream
+    for (auto &slot : s.pipe_ev) hip_check(hipEventRecord(slot[D2H], s.pipe_d2h), "stripe event");
+    h2d(0);
+    if (nstripes > 1) h2d(1);
+    if (g_prof.on) g_prof.ncall++;
+    for (size_t k = 0; k < nstripes; ++k) {
+        if (k + 2 < nstripes) h2d(k + 2);
+        const int sl = (int)(k % 3);
+        size_t len, first, np;
+        geom(k, &len, &first, &np);
+        const size_t m = len * np;  // elements of this stripe's ring
+        char *slot = slots + (size_t)sl * slot_bytes;
+        hip_check(hipStreamWaitEvent(s.stream, s.pipe_ev[sl][H2D], 0), "stripe wait");
+        const unsigned mis = (unsigned)((uintptr_t)slot & 15);
+        const Plan &p = cached_plan(SOSX_ALG_RING, P, t.my_idx, m, ts, mis, mis);
+        char *scr = p.scratch_bytes ? (char *)scratch(p.scratch_bytes) : nullptr;
+        int rc;
+        if (p2p) {
+            const size_t off = (size_t)(slot - s.sym_stage);
+            P2PBufs pb{slot, slot, scr, off, off, 0, mis, mis};
+            rc = p2p_exec(p, t, SOSX_ALG_RING, m, ts, pb, op, dt, s.stream);
+        } else {
+            Bufs b{slot, slot, scr};
+            rc = exec_rccl(p, t, b, op, dt, s.stream);
+        }
+        if (rc) raise_error("%s: %s", fn, status_text(rc));
+        hip_check(hipEventRecord(s.pipe_ev[sl][XCH], s.stream), "stripe event");
+        hip_check(hipStreamWaitEvent(s.pipe_d2h, s.pipe_ev[sl][XCH], 0), "stripe wait");
+        for (size_t c = 0; c < np; ++c)
+            hip_check(hipMemcpyAsync(dst + (disp(c) + first) * ts, slot + c * len * ts, len * ts,
+                                     hipMemcpyDeviceToHost, s.pipe_d2h), "stripe D2H");
+        hip_check(hipEventRecord(s.pipe_ev[sl][D2H], s.pipe_d2h), "stripe event");
+    }
+    hip_check(hipStreamSynchronize(s.pipe_d2h), fn);
+    hip_check(hipStreamSynchronize(s.stream), fn);
+    if (g_prof.on) g_prof.collect();
+    return true;
+}
+
 // Run plan `alg` (a reduction SOSX_ALG_*, a scan or a broadcast, plan.h) for this PE
 // over team t, on the library stream; returns when the call is complete.
 void execute(int alg, void *target, const void *source, size_t count, size_t ts, const Team &t,
@@ -226,6 +362,7 @@ void execute(int alg, void *target, const void *source, size_t count, size_t ts,
     State &s = st();
     const size_t bytes = count * ts;
     int rc;
+    if (striped_host_ring(alg, target, source, count, ts, t, op, dt, fn)) return;
     if (s.transport == TRANSPORT_P2P) {
         // buffers must live in the IPC-mapped device heap; anything else is staged
         // through this PE's stage region (in place), whose offset is published

@@ -155,6 +155,8 @@ static void read_env(State &s)
     if (t && strcmp(t, "p2p") && strcmp(t, "rccl") && strcmp(t, "both"))
         warn("Ignoring bad SHMEMX_TRANSPORT '%s'", t);
     s.dev_heap_bytes = atol_scaled(getenv("SHMEMX_DEVICE_HEAP_SIZE"), 2ull << 30);
+    s.host_stripe_bytes = atol_scaled(getenv("SHMEMX_HOST_STRIPE_BYTES"), 4u << 20);
+    s.host_stripe_explicit = getenv("SHMEMX_HOST_STRIPE_BYTES") != nullptr;
     s.sym_stage_bytes = atol_scaled(getenv("SHMEMX_STAGE_BYTES"), 512ull << 20);
     s.sym_stage_bytes = (s.sym_stage_bytes + 4095) & ~(size_t)4095;
     if (s.sym_stage_bytes >= s.dev_heap_bytes) s.dev_heap_bytes = s.sym_stage_bytes + (256u << 20);
@@ -572,6 +574,18 @@ void shmem_finalize(void)
     s.scratch_bytes = s.stage_bytes = 0;
     s.dbar = nullptr;
     sosx_combine_host_release();
+    if (s.stripes) (void)hipFree(s.stripes);
+    s.stripes = nullptr;
+    s.stripes_bytes = 0;
+    for (auto &slot : s.pipe_ev)
+        for (hipEvent_t &e : slot) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
+    for (hipStream_t *ps : {&s.pipe_h2d, &s.pipe_d2h}) {
+        if (*ps) (void)hipStreamDestroy(*ps);
+        *ps = nullptr;
+    }
     if (s.host_heap.base) (void)hipHostFree(s.host_heap.base);
     for (size_t q = 0; q < s.peer_heap.size(); ++q)
         if ((int)q != s.my_pe && s.peer_heap[q]) (void)hipIpcCloseMemHandle(s.peer_heap[q]);

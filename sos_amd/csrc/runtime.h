@@ -79,6 +79,14 @@ struct State {
     void *stage = nullptr;            // staging for host-resident source/target
     size_t stage_bytes = 0;
     int *dbar = nullptr;              // 1-int device word for barriers
+    // host-resident ring reductions, pipelined in stripes (collectives.cpp): copy streams,
+    // per-slot events, three device stripe slots (the RCCL path's; p2p uses the stage)
+    hipStream_t pipe_h2d = nullptr, pipe_d2h = nullptr;
+    hipEvent_t pipe_ev[3][3] = {};    // [slot][h2d done, exchange done, d2h done]
+    void *stripes = nullptr;
+    size_t stripes_bytes = 0;
+    size_t host_stripe_bytes = 4u << 20;   // SHMEMX_HOST_STRIPE_BYTES: min piece (0 = off)
+    bool host_stripe_explicit = false;     // set in the environment
     Heap host_heap;                   // shmem_malloc (pinned host)
     Heap dev_heap;                    // shmemx_malloc_device / external HIP heap
     // device symmetric heap layout: [stage region | user allocations]

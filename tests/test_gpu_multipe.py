@@ -159,3 +159,22 @@ def test_ipc_heap_sizes_with_bit31(heap):
                        capture_output=True, text=True, timeout=90, env=env)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     assert r.stdout.count("PE done") == 2, r.stdout
+
+
+@pytest.mark.parametrize("np_", [2, 3, 8])
+def test_team_check_host_stripes(np_):
+    """Host-resident ring reductions pipelined in stripes (striped_host_ring): with 256-B
+    chunk slices the host-buffer calls of tools/team_check.py run as many stripes plus
+    the n mod P remainder stripe (p2p stripes only when SHMEMX_HOST_STRIPE_BYTES is set),
+    bit for bit against the schedule-order fold."""
+    env_keep = os.environ.get("SHMEMX_HOST_STRIPE_BYTES")
+    os.environ["SHMEMX_HOST_STRIPE_BYTES"] = "256"
+    try:
+        r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900)
+    finally:
+        if env_keep is None:
+            os.environ.pop("SHMEMX_HOST_STRIPE_BYTES")
+        else:
+            os.environ["SHMEMX_HOST_STRIPE_BYTES"] = env_keep
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
+    assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
