@@ -243,18 +243,18 @@ bool striped_host_ring(int alg, void *target, const void *source, size_t count, 
     if (alg != SOSX_ALG_RING || P < 2 || P > SOSX_MAX_FOLD || s.host_stripe_bytes == 0) return false;
     if (is_device_ptr(source) || is_device_ptr(target)) return false;
     const size_t q = count / (size_t)P, r = count % (size_t)P;
-    // Stripe shape, from measurements of this stream/event pattern on MI355X with HIP 7.0
-    // (tools/diag/stripe_probe.py): pinned copies under ~4 MiB, or more than ~16 stripes
-    // in flight, make the runtime serialise the three streams (a 512 MiB pass at 32
-    // stripes took 2x the serial time); at <= 8 stripes of >= 4 MiB pieces a pass took
-    // 0.67x.  So: pieces of >= SHMEMX_HOST_STRIPE_BYTES (default 4 MiB), at most 8
-    // stripes.  The p2p executor synchronises the host every round, which leaves the copy
-    // streams little to overlap: it stripes only when SHMEMX_HOST_STRIPE_BYTES is set
-    // explicitly (the tests use tiny stripes to exercise the decomposition).
+    // Stripe shape, from measurements of this copy pattern on MI355X with HIP 7.0
+    // (tools/diag/stripe_copy_probe.py, profiles/r2_stripe_probe.txt): with 2-D copies a
+    // 512 MiB pass takes 0.62x the serial time at 8-16 stripes, a 64 MiB pass 0.72x even
+    // with 0.5 MiB slices.  So: slices of >= SHMEMX_HOST_STRIPE_BYTES (default 256 KiB),
+    // at most 16 stripes.  The p2p executor synchronises the host every round, which
+    // leaves the copy streams little to overlap: it stripes only when
+    // SHMEMX_HOST_STRIPE_BYTES is set explicitly (the tests use tiny stripes to exercise
+    // the decomposition).
     const bool p2p = s.transport == TRANSPORT_P2P;
     if (p2p && !s.host_stripe_explicit) return false;
     size_t L = (s.host_stripe_bytes + ts - 1) / ts;
-    if (!s.host_stripe_explicit) L = std::max(L, (q + 7) / 8);
+    if (!s.host_stripe_explicit) L = std::max(L, (q + 15) / 16);
     if (p2p) {  // three slots in the IPC-mapped stage region
         const size_t lim = s.sym_stage_bytes / 3 / ((size_t)P * ts);
         if (lim < L) L = lim;
@@ -304,15 +304,36 @@ bool striped_host_ring(int alg, void *target, const void *source, size_t count, 
     };
     const char *src = (const char *)source;
     char *dst = (char *)target;
+    // The np slices of a stripe, packed in the slot at len-element spacing, sit in the
+    // host vector at ring-chunk spacing: (q+1) elements for chunks c < r, q after.  So a
+    // stripe moves as at most two 2-D copies (hipMemcpy2DAsync), not np 1-D ones: the
+    // runtime pipelines a few large rectangular copies well and many small 1-D copies
+    // badly (profiles/r2_stripe_probe.txt).
+    auto copy_slices = [&](char *slot, char *host, size_t first, size_t len, size_t np,
+                           bool to_dev, hipStream_t strm) {
+        const size_t lo = np < r ? np : r;  // slices of the longer chunks, then the others
+        const size_t groups[2][2] = {{0, lo}, {lo, np}};
+        for (const auto &g : groups) {
+            const size_t c0 = g[0], rows = g[1] - g[0];
+            if (!rows) continue;
+            const size_t hpitch = (c0 < r ? q + 1 : q) * ts;
+            char *h = host + (disp(c0) + first) * ts;
+            char *d = slot + c0 * len * ts;
+            const hipError_t e =
+                to_dev ? hipMemcpy2DAsync(d, len * ts, h, hpitch, len * ts, rows,
+                                          hipMemcpyHostToDevice, strm)
+                       : hipMemcpy2DAsync(h, hpitch, d, len * ts, len * ts, rows,
+                                          hipMemcpyDeviceToHost, strm);
+            hip_check(e, to_dev ? "stripe H2D" : "stripe D2H");
+        }
+    };
     auto h2d = [&](size_t k) {
         const int sl = (int)(k % 3);
         size_t len, first, np;
         geom(k, &len, &first, &np);
         char *slot = slots + (size_t)sl * slot_bytes;
         hip_check(hipStreamWaitEvent(s.pipe_h2d, s.pipe_ev[sl][D2H], 0), "stripe wait");
-        for (size_t c = 0; c < np; ++c)
-            hip_check(hipMemcpyAsync(slot + c * len * ts, src + (disp(c) + first) * ts, len * ts,
-                                     hipMemcpyHostToDevice, s.pipe_h2d), "stripe H2D");
+        copy_slices(slot, (char *)src, first, len, np, true, s.pipe_h2d);
         hip_check(hipEventRecord(s.pipe_ev[sl][H2D], s.pipe_h2d), "stripe event");
     };
     // every slot starts free: its "D2H done" event is recorded on the idle copy stream
@@ -343,9 +364,7 @@ bool striped_host_ring(int alg, void *target, const void *source, size_t count, 
         if (rc) raise_error("%s: %s", fn, status_text(rc));
         hip_check(hipEventRecord(s.pipe_ev[sl][XCH], s.stream), "stripe event");
         hip_check(hipStreamWaitEvent(s.pipe_d2h, s.pipe_ev[sl][XCH], 0), "stripe wait");
-        for (size_t c = 0; c < np; ++c)
-            hip_check(hipMemcpyAsync(dst + (disp(c) + first) * ts, slot + c * len * ts, len * ts,
-                                     hipMemcpyDeviceToHost, s.pipe_d2h), "stripe D2H");
+        copy_slices(slot, dst, first, len, np, false, s.pipe_d2h);
         hip_check(hipEventRecord(s.pipe_ev[sl][D2H], s.pipe_d2h), "stripe event");
     }
     hip_check(hipStreamSynchronize(s.pipe_d2h), fn);

@@ -155,7 +155,7 @@ static void read_env(State &s)
     if (t && strcmp(t, "p2p") && strcmp(t, "rccl") && strcmp(t, "both"))
         warn("Ignoring bad SHMEMX_TRANSPORT '%s'", t);
     s.dev_heap_bytes = atol_scaled(getenv("SHMEMX_DEVICE_HEAP_SIZE"), 2ull << 30);
-    s.host_stripe_bytes = atol_scaled(getenv("SHMEMX_HOST_STRIPE_BYTES"), 4u << 20);
+    s.host_stripe_bytes = atol_scaled(getenv("SHMEMX_HOST_STRIPE_BYTES"), 256u << 10);
     s.host_stripe_explicit = getenv("SHMEMX_HOST_STRIPE_BYTES") != nullptr;
     s.sym_stage_bytes = atol_scaled(getenv("SHMEMX_STAGE_BYTES"), 512ull << 20);
     s.sym_stage_bytes = (s.sym_stage_bytes + 4095) & ~(size_t)4095;

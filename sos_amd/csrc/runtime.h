@@ -85,7 +85,7 @@ struct State {
     hipEvent_t pipe_ev[3][3] = {};    // [slot][h2d done, exchange done, d2h done]
     void *stripes = nullptr;
     size_t stripes_bytes = 0;
-    size_t host_stripe_bytes = 4u << 20;   // SHMEMX_HOST_STRIPE_BYTES: min piece (0 = off)
+    size_t host_stripe_bytes = 256u << 10; // SHMEMX_HOST_STRIPE_BYTES: min slice (0 = off)
     bool host_stripe_explicit = false;     // set in the environment
     Heap host_heap;                   // shmem_malloc (pinned host)
     Heap dev_heap;                    // shmemx_malloc_device / external HIP heap
