@@ -81,6 +81,7 @@ extern "C" {
 #define SOSX_ALG_RING       2  /* ring fold order (src/collectives.c:647-764), direct exchange  */
 #define SOSX_ALG_RECHALVING 3  /* recursive halving + doubling, recdbl_sw tree, pairwise xGMI  */
 #define SOSX_ALG_RECDBL_DIRECT 4 /* recdbl_sw tree evaluated by the owner after a direct exchange */
+#define SOSX_ALG_RECDBL_GATHER 5 /* recdbl_sw, every PE's own tree, after ONE all-gather round */
 
 /* ---- synthetic input distributions ------------------------ */
 #define SOSX_DIST_UNIFORM 0  /* fp: uniform [-1,1); ints: full-range random bits      */

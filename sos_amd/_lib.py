@@ -25,7 +25,7 @@ DTYPES = {
 }
 
 ORDER_LINEAR, ORDER_TREE = 0, 1
-ALGS = {"auto": 0, "recdbl": 1, "ring": 2, "rechalving": 3, "recdbl_direct": 4,
+ALGS = {"auto": 0, "recdbl": 1, "ring": 2, "rechalving": 3, "recdbl_direct": 4, "recdbl_gather": 5,
         "inscan": 16, "exscan": 17}
 PLAN_INSCAN, PLAN_EXSCAN = 16, 17
 

@@ -157,6 +157,60 @@ int build_recdbl(int P, int me, uint64_t count, uint64_t ts, unsigned dst_mis, P
     return SOSX_OK;
 }
 
+// recdbl_sw's result for every PE after ONE direct all-gather round (the latency-bound
+// small-message case: 1 exchange round instead of log2(P), + 2 for a non-power-of-2 P).
+// recdbl_sw at PE me < p2 (src/collectives.c:878-963) computes
+//   v[x] = in[x] OP in[x + p2] for x < P - p2, else in[x]        (fold of the extra PEs)
+//   T(x, 0) = v[x];  T(x, l) = T(x, l-1) OP T(x ^ 2^(l-1), l-1)   (left operand = own)
+// and hands T(me, log2 p2) to its extra partner me + p2.  Relabelling y = x ^ me turns
+// T(me, .) into the standard left-to-right pairwise tree over w[y] = v[y ^ me], which is
+// the fold kernel's TREE order over p2 inputs: so every PE evaluates ITS OWN recdbl_sw
+// expression (NaN payloads and +-0 ties included) from the gathered inputs, bit for bit.
+int build_recdbl_gather(int P, int me, uint64_t count, uint64_t ts, unsigned dst_mis, Plan *plan)
+{
+    const int p2 = pow2_floor(P);
+    const int nx = P - p2;  // extra PEs
+    if (p2 > SOSX_MAX_FOLD) return SOSX_ERR_ARG;
+    const uint64_t bytes = count * ts;
+    const uint64_t soff = dst_mis & 15;  // scratch slots congruent with DST
+    const uint64_t stride = round_up(bytes + 16, 256);
+    // slots: P-1 received vectors (indexed by distance), then nx pre-folded extras
+    auto rslot = [&](int pe) { return (uint64_t)((pe - me - 1 + P) % P) * stride + soff; };
+    auto vslot = [&](int x) { return (uint64_t)(P - 1 + x) * stride + soff; };
+    plan->scratch_bytes = (uint64_t)(P - 1 + nx) * stride;
+    auto in_buf = [&](int pe) { return pe == me ? SRC : SCR; };
+    auto in_off = [&](int pe) { return pe == me ? (uint64_t)0 : rslot(pe); };
+    Round r;
+    for (int k = 1; k < P; ++k) {
+        const int peer = (me + k) % P;
+        r.xfers.push_back(xf(1, peer, SRC, 0, bytes));
+        r.xfers.push_back(xf(0, peer, SCR, rslot(peer), bytes));
+    }
+    for (int x = 0; x < nx; ++x)
+        r.ops.push_back(fold2(SCR, vslot(x), in_buf(x), in_off(x), in_buf(x + p2), in_off(x + p2),
+                              count));
+    const int mp = me < p2 ? me : me - p2;  // an extra PE receives its partner's result
+    Local l;
+    memset(&l, 0, sizeof(l));
+    l.kind = FOLD;
+    l.order = SOSX_ORDER_TREE;
+    l.out_buf = DST;
+    l.out_off = 0;
+    l.nin = p2;
+    l.count = count;
+    for (int y = 0; y < p2; ++y) {
+        const int x = y ^ mp;
+        l.in_buf[y] = x < nx ? SCR : in_buf(x);
+        l.in_off[y] = x < nx ? vslot(x) : in_off(x);
+    }
+    if (p2 == 1) {  // P == 1 is handled by build(); P >= 2 always has p2 >= 2
+        return SOSX_ERR_ARG;
+    }
+    r.ops.push_back(l);
+    plan->rounds.push_back(r);
+    return SOSX_OK;
+}
+
 // Recursive halving (reduce-scatter at distance 1, 2, 4, ...) + recursive doubling
 // (allgather at distance ..., 4, 2, 1), with the recdbl_sw fold of extra PEs.
 int build_rechalving(int P, int me, uint64_t count, uint64_t ts, unsigned dst_mis, Plan *plan)
@@ -393,7 +447,9 @@ void ring_chunk(uint64_t count, int P, int c, uint64_t *n, uint64_t *first)
 
 int resolve_alg(int alg, uint64_t bytes, uint64_t crossover)
 {
-    if (alg == SOSX_ALG_AUTO) return bytes < crossover ? SOSX_ALG_RECDBL : SOSX_ALG_RING;
+    // below the crossover SOS runs recdbl_sw; the one-round gather form gives the same
+    // bits with fewer exchange rounds
+    if (alg == SOSX_ALG_AUTO) return bytes < crossover ? SOSX_ALG_RECDBL_GATHER : SOSX_ALG_RING;
     return alg;
 }
 
@@ -445,6 +501,8 @@ int build(int alg, int P, int me, uint64_t count, uint64_t ts, unsigned src_mis,
             return build_direct(alg, P, me, count, ts, src_mis, dst_mis, out);
         case SOSX_ALG_RECDBL:
             return build_recdbl(P, me, count, ts, dst_mis, out);
+        case SOSX_ALG_RECDBL_GATHER:
+            return build_recdbl_gather(P, me, count, ts, dst_mis, out);
         case SOSX_ALG_RECHALVING:
             return build_rechalving(P, me, count, ts, dst_mis, out);
         default:

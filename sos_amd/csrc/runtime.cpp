@@ -128,6 +128,7 @@ int parse_reduce_alg(const char *type, int dflt)
     if (!strcmp(type, "ring")) return SOSX_ALG_RING;
     if (!strcmp(type, "rechalving")) return SOSX_ALG_RECHALVING;
     if (!strcmp(type, "recdbl_direct")) return SOSX_ALG_RECDBL_DIRECT;
+    if (!strcmp(type, "recdbl_gather")) return SOSX_ALG_RECDBL_GATHER;
     warn("Ignoring bad reduction algorithm '%s'", type);
     return dflt;
 }
@@ -789,7 +790,7 @@ int shmemx_set_transport(int transport)
 int shmemx_set_reduce_algorithm(int alg)
 {
     int prev = st().reduce_alg;
-    if (alg >= SOSX_ALG_AUTO && alg <= SOSX_ALG_RECDBL_DIRECT) st().reduce_alg = alg;
+    if (alg >= SOSX_ALG_AUTO && alg <= SOSX_ALG_RECDBL_GATHER) st().reduce_alg = alg;
     return prev;
 }
 

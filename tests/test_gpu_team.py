@@ -32,7 +32,7 @@ CASES = [(23, 5, 0), (24, 6, 1), (11, 2, 0), (4, 4, 0), (18, 3, 0), (27, 6, 1), 
          (1, 5, 0), (10, 0, 0)]
 
 
-@pytest.mark.parametrize("alg", ["ring", "recdbl", "rechalving", "recdbl_direct", "auto"])
+@pytest.mark.parametrize("alg", ["ring", "recdbl", "rechalving", "recdbl_direct", "recdbl_gather", "auto"])
 @pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 8])
 def test_loopback_schedules(torch_cuda, sos, oracle, alg, P):
     from sos_amd import shmem as S
@@ -55,7 +55,7 @@ def test_loopback_schedules(torch_cuda, sos, oracle, alg, P):
                                      [b.data_ptr() + pad for b in db], n)
                 torch.cuda.synchronize()
                 for p in range(P):
-                    want = ref[p] if alg in ("ring", "recdbl", "auto") else ref[0]
+                    want = ref[p] if alg in ("ring", "recdbl", "recdbl_gather", "auto") else ref[0]
                     got = host_view(db[p], pad, srcs[p])
                     assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), \
                         (alg, P, dt, op, n, in_place, p)

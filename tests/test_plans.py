@@ -2,6 +2,7 @@
 
   ring          == SOS ring (src/collectives.c:647-764) bit for bit, every type/op
   recdbl        == SOS recdbl_sw (src/collectives.c:850-984) bit for bit, per PE
+  recdbl_gather == SOS recdbl_sw bit for bit, per PE, after one all-gather round
   rechalving    == SOS recdbl_sw for commutative element semantics
   recdbl_direct == SOS recdbl_sw for commutative element semantics
 Also: SOS AUTO crossover, chunk math, in-place calls, ragged/empty chunks.
@@ -43,15 +44,16 @@ def test_ring_plan_matches_sos_ring(P, dt, op, dist):
             assert np.array_equal(bits(got[p]), bits(ref[p])), (P, n, p)
 
 
-@pytest.mark.parametrize("P", [2, 3, 4, 6, 8])
+@pytest.mark.parametrize("alg", ["recdbl", "recdbl_gather"])
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("dt,op,dist", CASES)
-def test_recdbl_plan_matches_sos_recdbl(P, dt, op, dist):
+def test_recdbl_plan_matches_sos_recdbl(alg, P, dt, op, dist):
     for n in (1, 7, 300):
         srcs = [O.fill(dt, dist, 3 + n, p, n) for p in range(P)]
         ref = O.recdbl(op, dt, srcs)
-        got = plansim.simulate("recdbl", op, dt, srcs)
+        got = plansim.simulate(alg, op, dt, srcs)
         for p in range(P):
-            assert np.array_equal(bits(got[p]), bits(ref[p])), (P, n, p)
+            assert np.array_equal(bits(got[p]), bits(ref[p])), (alg, P, n, p)
 
 
 @pytest.mark.parametrize("alg", ["rechalving", "recdbl_direct"])
@@ -67,34 +69,43 @@ def test_tree_plans_match_sos_recdbl(alg, P, dt, op, dist):
             assert np.array_equal(bits(got[p]), bits(ref[0])), (alg, P, n, p)
 
 
-@pytest.mark.parametrize("alg", ["ring", "recdbl", "rechalving", "recdbl_direct"])
+@pytest.mark.parametrize("alg", ["ring", "recdbl", "rechalving", "recdbl_direct", "recdbl_gather"])
 def test_in_place(alg):
     P, n, dt, op = 5, 333, 23, 5
     srcs = [O.fill(dt, 0, 77, p, n) for p in range(P)]
     ref = O.ring(op, dt, srcs) if alg == "ring" else O.recdbl(op, dt, srcs)
     got = plansim.simulate(alg, op, dt, srcs, in_place=True)
     for p in range(P):
-        assert np.array_equal(bits(got[p]), bits(ref[p if alg in ("ring", "recdbl") else 0]))
+        assert np.array_equal(bits(got[p]),
+                              bits(ref[p if alg in ("ring", "recdbl", "recdbl_gather") else 0]))
 
 
-def test_minmax_ties_recdbl_per_pe():
-    """fp max with +-0 ties and NaNs: recdbl keeps every PE's own perspective."""
-    P, n = 4, 64
-    rng = np.random.default_rng(3)
-    pool = np.array([0.0, -0.0, np.nan, 1.0, -1.0], dtype=np.float32)
+@pytest.mark.parametrize("alg", ["recdbl", "recdbl_gather"])
+@pytest.mark.parametrize("P", [3, 4, 6, 8])
+@pytest.mark.parametrize("op", [3, 4, 5])
+def test_minmax_ties_recdbl_per_pe(alg, P, op):
+    """fp min/max/sum with +-0 ties and NaNs: recdbl keeps every PE's own perspective."""
+    n = 256
+    rng = np.random.default_rng(3 + P)
+    pool = np.array([0.0, -0.0, np.nan, -np.nan, 1.0, -1.0], dtype=np.float32)
     srcs = [rng.choice(pool, n).astype(np.float32) for _ in range(P)]
-    ref = O.recdbl(4, 23, srcs)
-    got = plansim.simulate("recdbl", 4, 23, srcs)
+    # distinct NaN payloads per PE, so the x86 first-operand NaN rule shows too
+    for p, a in enumerate(srcs):
+        v = a.view(np.uint32)
+        v[np.isnan(a)] |= np.uint32(p + 1)
+    ref = O.recdbl(op, 23, srcs)
+    got = plansim.simulate(alg, op, 23, srcs)
     for p in range(P):
-        assert np.array_equal(bits(got[p]), bits(ref[p]))
+        assert np.array_equal(bits(got[p]), bits(ref[p])), (alg, P, op, p)
     # and the PEs genuinely disagree (perspective matters), so the check has teeth
     assert any(not np.array_equal(bits(ref[0]), bits(ref[p])) for p in range(1, P))
 
 
 def test_auto_crossover():
-    # SOS AUTO without NIC atomics: recdbl below COLL_SIZE_CROSSOVER (16 KiB), else ring
+    # SOS AUTO without NIC atomics: recdbl_sw below COLL_SIZE_CROSSOVER (16 KiB), else ring;
+    # the recdbl_sw results come from the one-round gather form (same bits per PE)
     lib = S.lib()
-    assert lib.sosx_resolve_alg(0, 16383, 16384) == 1
+    assert lib.sosx_resolve_alg(0, 16383, 16384) == 5
     assert lib.sosx_resolve_alg(0, 16384, 16384) == 2
     assert lib.sosx_resolve_alg(3, 16, 16384) == 3
 
@@ -125,3 +136,7 @@ def test_wire_bytes():
             pl = S.plan(alg, P, 0, n, ts)
             sent = sum(x["bytes"] for rd in pl["rounds"] for x in rd["xfers"] if x["send"])
             assert sent == expect, (alg, P, sent, expect)
+        pl = S.plan("recdbl_gather", P, 0, n, ts)
+        assert len(pl["rounds"]) == 1  # one exchange round whatever P
+        sent = sum(x["bytes"] for rd in pl["rounds"] for x in rd["xfers"] if x["send"])
+        assert sent == (P - 1) * n * ts

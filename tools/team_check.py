@@ -22,7 +22,7 @@ from sos_amd import shmem as S  # noqa: E402
 
 CASES = [("float", "sum"), ("double", "prod"), ("int64", "xor"), ("int", "max"), ("complexd", "prod"),
          ("short", "sum"), ("uint8", "min"), ("ulong", "or")]
-ALGS = ["auto", "ring", "recdbl", "rechalving", "recdbl_direct"]
+ALGS = ["auto", "ring", "recdbl", "rechalving", "recdbl_direct", "recdbl_gather"]
 SIZES = [1, 37, 5003, (1 << 20) + 3]
 
 
