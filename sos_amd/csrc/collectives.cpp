@@ -241,7 +241,6 @@ bool striped_host_ring(int alg, void *target, const void *source, size_t count, 
     State &s = st();
     const int P = t.size;
     if (alg != SOSX_ALG_RING || P < 2 || P > SOSX_MAX_FOLD || s.host_stripe_bytes == 0) return false;
-    if (is_device_ptr(source) || is_device_ptr(target)) return false;
     const size_t q = count / (size_t)P, r = count % (size_t)P;
     // Stripe shape, from measurements of this copy pattern on MI355X with HIP 7.0
     // (tools/diag/stripe_copy_probe.py, profiles/r2_stripe_probe.txt): with 2-D copies a
@@ -260,6 +259,8 @@ bool striped_host_ring(int alg, void *target, const void *source, size_t count, 
         if (lim < L) L = lim;
     }
     if (L == 0 || q < 2 * L) return false;
+    // only now the (costlier) residency queries: both operands must be host memory
+    if (is_device_ptr(source) || is_device_ptr(target)) return false;
     const size_t slot_bytes = ((size_t)P * L * ts + 255) / 256 * 256;
     char *slots;
     if (p2p) {
