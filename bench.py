@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--sweep", action="store_true",
                    help="SURVEY 8(d) config #5 roofline scan of the combine kernel instead of "
                         "the headline line (N=1)")
+    p.add_argument("--sweep-pairs", default="configs",
+                   help="'configs' (SURVEY 8(d) #2/#3/#5) or 'all' (every datatype class)")
+    p.add_argument("--sweep-min", type=int, default=1 << 10)
     p.add_argument("--sweep-max", type=int, default=256 << 20,
                    help="largest nreduce of the N=1 sweep and of the N>1 size curve")
     p.add_argument("--no-team-sweep", action="store_true",
@@ -303,6 +306,11 @@ def variants_ab(args, torch, L, launch):
 
 
 # config #5 (and #2, #3): (type, op) pairs of the roofline scan
+SWEEP_ALL = [("char", "sum"), ("schar", "max"), ("short", "prod"), ("uchar", "xor"),
+             ("ushort", "min"), ("uint", "sum"), ("long", "and"), ("ulong", "max"),
+             ("ptrdiff", "sum"), ("size", "prod"), ("float", "max"), ("float", "prod"),
+             ("complexf", "sum"), ("complexf", "prod"), ("longdouble", "sum"),
+             ("longdouble", "max")]
 SWEEP_PAIRS = [("int", "min"), ("int", "max"), ("int", "prod"),
                ("double", "min"), ("double", "max"), ("double", "prod"), ("double", "sum"),
                ("complexd", "prod"), ("complexd", "sum"),
@@ -323,12 +331,12 @@ def sweep(args, torch):
     stream = torch.cuda.current_stream()
     S = stream.cuda_stream
     sizes = []
-    n = 1 << 10
+    n = args.sweep_min
     while n <= args.sweep_max:
         sizes.append(n)
         n *= 4
     rows = []
-    for tname, oname in SWEEP_PAIRS:
+    for tname, oname in (SWEEP_PAIRS if args.sweep_pairs == "configs" else SWEEP_ALL):
         dt, op = L.dtype_id(tname), L.op_id(oname)
         es = L.dtype_size(dt)
         dist = L.DIST_PROD if oname == "prod" else L.DIST_UNIFORM
@@ -336,9 +344,20 @@ def sweep(args, torch):
         a = torch.empty(nmax * es, dtype=torch.uint8, device="cuda")
         b = torch.empty_like(a)
         c = torch.empty_like(a)
+        ld_src = None
+        if tname == "longdouble":  # no device generator for x87 values: host-made, uploaded
+            import numpy as np
+            rng = np.random.default_rng(SEED)
+            v = (rng.uniform(0.5, 2.0, (2, nmax)) if oname == "prod"
+                 else rng.standard_normal((2, nmax))).astype(np.longdouble)
+            ld_src = [torch.from_numpy(v[k].view(np.uint8).copy()).cuda() for k in range(2)]
         for n in sizes:
-            L.fill(dt, dist, SEED, 0, a.data_ptr(), n, 0, S)
-            L.fill(dt, dist, SEED, 1, b.data_ptr(), n, 0, S)
+            if ld_src is not None:
+                a[:n * es].copy_(ld_src[0][:n * es])
+                b[:n * es].copy_(ld_src[1][:n * es])
+            else:
+                L.fill(dt, dist, SEED, 0, a.data_ptr(), n, 0, S)
+                L.fill(dt, dist, SEED, 1, b.data_ptr(), n, 0, S)
             # check first: fold(a, b) -> c, then combine a OP= b, compare
             L.fold(op, dt, L.ORDER_LINEAR, c.data_ptr(), [a.data_ptr(), b.data_ptr()], n, S)
             L.combine(op, dt, a.data_ptr(), b.data_ptr(), n, S)
