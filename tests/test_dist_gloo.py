@@ -77,6 +77,8 @@ def _worker(rank, world, port, alg, dt, op, n, in_place, outq):
     (3, "ring", 11, 2, 777, True),
     (4, "ring", 27, 6, 513, False),
     (3, "recdbl", 23, 4, 200, False),
+    (3, "recdbl_gather", 23, 4, 200, False),
+    (4, "recdbl_gather", 24, 6, 333, True),
     (2, "rechalving", 24, 5, 1001, False),
     (3, "rechalving", 11, 5, 99, True),
     (4, "recdbl_direct", 10, 6, 640, False),
@@ -98,5 +100,5 @@ def test_plans_across_processes(world, alg, dt, op, n, in_place):
     srcs = [O.fill(dt, 1 if op == 6 else 0, 1000 + n, r, n) for r in range(world)]
     ref = O.ring(op, dt, srcs) if alg == "ring" else O.recdbl(op, dt, srcs)
     for r in range(world):
-        want = ref[r] if alg in ("ring", "recdbl") else ref[0]
+        want = ref[r] if alg in ("ring", "recdbl", "recdbl_gather") else ref[0]
         assert got[r] == want.tobytes(), (alg, world, r)
