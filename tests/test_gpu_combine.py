@@ -312,3 +312,26 @@ def test_every_combine_variant_bit_exact(torch_cuda, sos, oracle):
                 assert same_bits(from_dev(da, off, a), ref), (v, off)
     finally:
         L.sosx_set_combine_variant(0)
+
+
+def test_combine_host_pipeline_release_and_regrow(torch_cuda, sos, oracle):
+    """The host pipeline's HBM slots: grown for a large chunk, reused for a smaller one,
+    released (sosx_combine_host_release, as shmem_finalize does) and set up again --
+    every call still bit-exact."""
+    import ctypes
+    L = sos.lib()
+    L.sosx_combine_host_release.restype = None
+    n = (1 << 21) + 5
+    a, b = oracle.fill(24, 0, 31, 0, n), oracle.fill(24, 0, 31, 1, n)
+    ref = a.copy()
+    oracle.reduce_local(5, 24, b, ref)
+    for chunk in (8 << 20, 1 << 20, 0, None, 4 << 20):
+        if chunk is None:
+            L.sosx_combine_host_release()
+            L.sosx_combine_host_release()  # idempotent
+            continue
+        got = a.copy()
+        rc = L.sosx_combine_host(5, 24, got.ctypes.data_as(ctypes.c_void_p),
+                                 b.ctypes.data_as(ctypes.c_void_p), n, chunk)
+        assert rc == 0
+        assert same_bits(got, ref), chunk
