@@ -127,6 +127,10 @@ def main(args, torch):
     curve = size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
                        src, dst, stream, sorted(sweep_sizes + [n]), results) if sweep_sizes else {}
 
+    schedules = {} if getattr(args, "no_adjacent", False) else \
+        other_schedules(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
+                        src, dst, stream, results)
+
     host_leg = {} if getattr(args, "no_host", False) else \
         host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank,
                            world, stream, results)
@@ -196,6 +200,8 @@ def main(args, torch):
                                "(SHMEMX_TRANSPORT selects)")
     if curve:
         res["size_curve"] = curve
+    if schedules:
+        res["schedules"] = schedules
     if host_leg:
         res["host_resident"] = host_leg
     if adjacent:
@@ -306,6 +312,57 @@ def size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank,
             log(f"[team curve] {tname} n={m} {row['ms_per_call']} ms/call {row['value_GiBs']} GiB/s "
                 f"busbw {row['busbw_GBs']} GB/s")
         out[tname] = rows
+    S.lib().shmemx_set_transport(0)
+    return out
+
+
+def other_schedules(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world, src,
+                    dst, stream, headline):
+    """The headline reduction under the other bit-exact-for-sum schedules
+    (SHMEM_REDUCE_ALGORITHM): the north star's recursive halving + doubling (pairwise,
+    one link per step) and recdbl_direct (recdbl_sw tree after a direct exchange), on each
+    transport, with the bitwise self-check (recdbl_sw tree order) on fresh inputs."""
+    n, P = args.n, world
+    out = {}
+    steps = max(3, min(args.steps, 10))
+    for tname, tid in (("rccl", 0), ("p2p", 1)):
+        if not headline.get(tname, {}).get("available", True) or S.lib().shmemx_set_transport(tid) < 0:
+            continue
+        for sname in ("rechalving", "recdbl_direct"):
+            alg = L.ALGS[sname]
+            S.shmemx_set_reduce_algorithm(alg)
+            if rank == 0:
+                log(f"[team] schedule {sname} on {tname}")
+            for _ in range(2):
+                fn(team, dst, src, n)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                fn(team, dst, src, n)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            el = torch.tensor([t1 - t0], dtype=torch.float64)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            ts = el.item() / steps
+            cseed = seed + 307 + tid
+            L.fill(dt, dist_kind, cseed, rank, src, n, 0, stream)
+            torch.cuda.synchronize()
+            dist.barrier()
+            fn(team, dst, src, n)
+            mm = self_check(torch, L, S, dt, L.op_id(args.op), dist_kind, cseed, world, n, es, alg,
+                            dst, stream)
+            mmt = torch.tensor([mm], dtype=torch.int64)
+            dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
+            L.fill(dt, dist_kind, seed, rank, src, n, 0, stream)
+            torch.cuda.synchronize()
+            wire = 2 * (P - 1) / P * n * es
+            out.setdefault(tname, {})[sname] = {
+                "ms_per_call": round(ts * 1e3, 4),
+                "value_GiBs": round(world * n * es / ts / GiB, 3),
+                "busbw_GBs": round(wire / ts / 1e9, 1),
+                "bitwise_mismatches_all_ranks": int(mmt.item())}
+    S.shmemx_set_reduce_algorithm(L.ALGS[args.alg])
     S.lib().shmemx_set_transport(0)
     return out
 

@@ -107,6 +107,8 @@ def test_bench_team_leg(np_):
     for coll in res.get("adjacent_collectives", {}).get("p2p", {}).values():
         assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]
     assert res["host_resident"]["p2p"]["value_GiBs"] > 0, res["host_resident"]
+    for sched in ("rechalving", "recdbl_direct"):
+        assert res["schedules"]["p2p"][sched]["bitwise_mismatches_all_ranks"] == 0, res["schedules"]
     curve = res["size_curve"]["p2p"]
     assert [r["nreduce"] for r in curve] == [1 << 20, (1 << 20) + 3, 4 << 20]
     assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
