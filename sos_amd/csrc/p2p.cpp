@@ -25,6 +25,8 @@
 // chunks -- the RCCL version's scratch round trip disappears.
 #include <time.h>
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -111,6 +113,25 @@ void spin_until(std::atomic<uint64_t> &a, uint64_t want, const char *what)
     }
 }
 
+// SOSX_P2P_TRACE=N (diagnostics): host time per phase of p2p_exec, averaged and printed
+// to stderr every N calls.
+struct Trace {
+    int every = -1;  // -1: not read yet, 0: off
+    double t[6] = {0, 0, 0, 0, 0, 0};
+    long calls = 0;
+};
+Trace g_trace;
+enum { PH_SYNC_SEND, PH_WAIT_POST, PH_ENQUEUE, PH_SYNC_OPS, PH_WAIT_CONSUMED, PH_SYNC_END };
+
+bool trace_on()
+{
+    if (g_trace.every < 0) {
+        const char *e = getenv("SOSX_P2P_TRACE");
+        g_trace.every = e ? atoi(e) : 0;
+    }
+    return g_trace.every > 0;
+}
+
 struct PeerSend {
     int buf;
     uint64_t off, bytes;
@@ -170,6 +191,14 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
                                 std::memory_order_relaxed);
     sh->pub[my_world].dst_off.store(b.dst_off, std::memory_order_release);
     std::vector<int> recv_idx((size_t)t.size, 0);  // k-th receive from each team peer
+    const bool tr = trace_on();
+    double tp = tr ? now_s() : 0;
+    auto phase = [&](int ph) {
+        if (!tr) return;
+        const double now = now_s();
+        g_trace.t[ph] += now - tp;
+        tp = now;
+    };
     auto local_ptr = [&](int buf, uint64_t off) -> char * {
         return (buf == sosplan::SRC ? (char *)b.src : buf == sosplan::DST ? b.dst : b.scr) + off;
     };
@@ -179,6 +208,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
         for (const auto &x : r.xfers) any_send |= x.send != 0;
         if (any_send) {
             if (hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
+            phase(PH_SYNC_SEND);
             for (const auto &x : r.xfers)
                 if (x.send) {
                     const int pw = t.world_rank(x.peer);
@@ -194,6 +224,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
             const int pw = t.world_rank(x.peer);
             const uint64_t want = ++g_local.seen_from[pw];
             spin_until(sh->posted[pw][my_world], want, "a peer's data");
+            phase(PH_WAIT_POST);
             const uint64_t dst_off = sh->pub[pw].dst_off.load(std::memory_order_acquire);
             const auto &sends = peer_sends(alg, t.size, x.peer, me, count, ts,
                                            sh->pub[pw].mis.load(std::memory_order_relaxed));
@@ -286,21 +317,34 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
             if (rc) return rc;
         }
         // 4. receives done -> consumed; wait for my sends to be consumed
+        phase(PH_ENQUEUE);
         if (!segs.empty() || fuse_ok) {
             if (hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
         }
+        phase(PH_SYNC_OPS);
         for (auto &sg : segs) sh->consumed[sg.peer_world][my_world].fetch_add(1, std::memory_order_release);
         for (const auto &x : r.xfers)
             if (x.send) {
                 const int pw = t.world_rank(x.peer);
                 spin_until(sh->consumed[my_world][pw], g_local.posted_by_me[pw], "a peer to read");
             }
+        phase(PH_WAIT_CONSUMED);
         if (!fuse_ok) {
             int rc = run_ops();
             if (rc) return rc;
         }
     }
-    return hipStreamSynchronize(stream) == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
+    const hipError_t e = hipStreamSynchronize(stream);
+    phase(PH_SYNC_END);
+    if (tr && ++g_trace.calls % g_trace.every == 0) {  // window averages, then reset
+        const double k = 1e6 / (double)g_trace.every;
+        fprintf(stderr, "[%04d] p2p trace (calls %ld-%ld, us/call): sync-send %.1f wait-post %.1f "
+                "enqueue %.1f sync-ops %.1f wait-consumed %.1f sync-end %.1f\n", s.my_pe,
+                g_trace.calls - g_trace.every + 1, g_trace.calls, g_trace.t[0] * k, g_trace.t[1] * k,
+                g_trace.t[2] * k, g_trace.t[3] * k, g_trace.t[4] * k, g_trace.t[5] * k);
+        for (double &v : g_trace.t) v = 0;
+    }
+    return e == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
 }
 
 }  // namespace sosrt
