@@ -420,7 +420,31 @@ static void init_common(int pe, int npes, const ncclUniqueId *uid)
     s.stream = s.own_stream;
     hip_check(hipMalloc((void **)&s.dbar, 64), "hipMalloc(barrier word)");
     hip_check(hipMemset(s.dbar, 0, 64), "hipMemset");
-    if (uid) nccl_check(ncclCommInitRank(&s.comm, npes, *uid, pe), "ncclCommInitRank");
+    if (uid) {
+        const ncclResult_t r = ncclCommInitRank(&s.comm, npes, *uid, pe);
+        // SHMEMX_TRANSPORT=both: an RCCL communicator that fails to come up leaves the
+        // job on the p2p transport (agreed over the bootstrap, so every PE switches)
+        const bool can_fall_back = s.want_p2p && s.hub.up && npes > 1;
+        if (r != ncclSuccess && !can_fall_back) nccl_check(r, "ncclCommInitRank");
+        if (r != ncclSuccess) {
+            warn("RCCL communicator init failed (%s)", ncclGetErrorString(r));
+            s.comm = nullptr;
+        }
+        if (can_fall_back) {
+            int ok = s.comm != nullptr;
+            std::vector<int> oks((size_t)npes);
+            if (sosboot::hub_allgather(&s.hub, &ok, sizeof(ok), oks.data()) != 0)
+                raise_error("shmem_init: RCCL status agreement failed");
+            for (int v : oks) ok &= v;
+            if (!ok) {
+                if (s.comm) (void)ncclCommDestroy(s.comm);
+                s.comm = nullptr;
+                s.want_rccl = false;
+                s.transport = TRANSPORT_P2P;
+                warn("RCCL unavailable on some PE: every PE runs on the p2p transport");
+            }
+        }
+    }
     s.world = Team();
     s.world.start = 0;
     s.world.stride = 1;

@@ -180,3 +180,28 @@ def test_team_check_host_stripes(np_):
             os.environ["SHMEMX_HOST_STRIPE_BYTES"] = env_keep
     ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
     assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
+
+
+def test_bench_team_leg_default_transport():
+    """bench.py's N > 1 default (SHMEMX_TRANSPORT=both, what the driver's 8-GPU run uses),
+    here with 2 ranks on one GPU: RCCL refuses a second rank on the device, so init falls
+    back -- on every PE, agreed over the bootstrap -- to the p2p transport, and the line
+    comes out with clean checks."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+              "SHMEMX_TRANSPORT"):
+        env.pop(k, None)
+    env.update({"SHMEMX_DEVICE": "0", "PYTHONPATH": ROOT})
+    port = 29700 + os.getpid() % 500
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--nreduce", str((1 << 20) + 3), "--sweep-max", str(4 << 20)],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    import json
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["config"]["transport"] == "p2p" and list(res["transports"]) == ["p2p"]
+    assert res["check"]["bitwise_mismatches_all_ranks"] == 0
+    assert "every PE runs on the p2p transport" in r.stderr
