@@ -10,6 +10,9 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libsos_amd.so")
+# Test hook: SOSX_LIBRARY names another build of the same library to load instead, e.g.
+# tests/fakerccl/libsos_amd_fakerccl.so, whose RCCL calls are bound to a file-based
+# stand-in so the RCCL executor can run with several PEs on one GPU (tests/test_gpu_fakerccl.py).
 
 # shm_internal_op_t (src/transport_none.h:25-33)
 OPS = {"and": 0, "or": 1, "xor": 2, "min": 3, "max": 4, "sum": 5, "prod": 6}
@@ -112,19 +115,20 @@ def lib():
     global _LIB
     if _LIB is not None:
         return _LIB
-    if not os.path.exists(LIB_PATH):
+    path = os.environ.get("SOSX_LIBRARY") or LIB_PATH
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            f"{path} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback for the SOS reduction path)")
     try:
         import torch  # noqa: F401  (maps torch's HIP runtime before ours is resolved)
     except ImportError:
         pass
     before = loaded_runtimes()
-    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     added = {k: v for k, v in loaded_runtimes().items() if len(v) > max(1, len(before[k]))}
     if added:
-        raise ImportError(f"loading {LIB_PATH} mapped a second copy of a ROCm runtime "
+        raise ImportError(f"loading {path} mapped a second copy of a ROCm runtime "
                           f"library: {added}")
     for name, (res, args) in _SIGS.items():
         fn = getattr(L, name, None)

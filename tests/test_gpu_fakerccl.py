@@ -1,0 +1,149 @@
+"""GPU, several PE processes on one MI355X: the RCCL executor end to end.
+
+Real RCCL refuses two ranks on one GPU, so these runs load a test build of the library,
+tests/fakerccl/libsos_amd_fakerccl.so: the same objects as sos_amd/libsos_amd.so, with the
+eight RCCL entry points it calls bound to tests/fakerccl/fake_rccl.cpp, which moves each
+ncclSend/ncclRecv through a /dev/shm file with RCCL's per-pair FIFO matching.  Everything
+above those calls is the product code the 8-GPU node runs with SHMEMX_TRANSPORT=rccl: the
+plans, exec_rccl's byte offsets and groups, the folds between rounds, the striped
+host-resident ring, the RCCL device barrier.  The checkers are the ones the p2p runs use
+(bit-exact against an on-GPU re-evaluation of each schedule's element order).
+"""
+import glob
+import json
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OSHRUN = os.path.join(ROOT, "tools", "oshrun")
+FAKE = os.path.join(ROOT, "tests", "fakerccl", "libsos_amd_fakerccl.so")
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update({"SOSX_LIBRARY": FAKE, "SHMEMX_TRANSPORT": "rccl", "SHMEMX_DEVICE": "0",
+                "SHMEMX_DEVICE_HEAP_SIZE": "256M", "FAKERCCL_TIMEOUT": "60", "FAKERCCL_STATS": "1", "PYTHONPATH": ROOT})
+    return env
+
+
+@pytest.fixture(autouse=True)
+def _no_leftover_messages():
+    assert os.path.exists(FAKE), "tests/fakerccl/libsos_amd_fakerccl.so is not built"
+    yield
+    left = glob.glob("/dev/shm/fakerccl_*")
+    for f in left:
+        os.unlink(f)
+    assert not left, f"unreceived messages: {left[:4]}"
+
+
+def oshrun(np_, cmd, timeout=600, **extra):
+    env = _env()
+    env.update(extra)
+    return subprocess.run([sys.executable, OSHRUN, "-np", str(np_), "--timeout", str(timeout - 30),
+                           *cmd], capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def _ok(r, np_):
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
+    assert sorted(int(p) for p in ok) == list(range(np_)), r.stdout[-3000:]
+    _used_fake(r, np_)
+
+
+def _used_fake(r, np_):
+    """Every rank moved data through the stand-in (so the RCCL executor ran) without error."""
+    assert "fakerccl error" not in r.stderr, r.stderr[-2000:]
+    sent = {int(rk): int(m) for rk, m in
+            re.findall(r"fakerccl stats: rank (\d+) sent (\d+) messages", r.stderr)}
+    assert sorted(sent) == list(range(np_)) and min(sent.values()) > 0, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("np_", [2, 3, 4])
+def test_team_check_rccl_executor(np_):
+    """Every schedule, 8 type/op pairs, heap / device / host buffers, in place, a split team."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900)
+    _ok(r, np_)
+
+
+@pytest.mark.parametrize("np_", [3])
+def test_coll_check_rccl_executor(np_):
+    """Scans and broadcasts over the RCCL executor."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "coll_check.py")], timeout=600)
+    _ok(r, np_)
+
+
+def test_team_management_rccl(np_=4):
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_mgmt_check.py")], timeout=300)
+    _ok(r, np_)
+
+
+def test_api_sweep_rccl(np_=2):
+    """All 154 typed reductions and 44 to_all entry points through the public API."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "api_sweep_pe.py")], timeout=600)
+    _ok(r, np_)
+
+
+def test_bench_team_leg_rccl():
+    """bench.py's N > 1 line as the driver runs it on the 8-GPU node, transport forced to
+    RCCL: the headline ring, the size curve, rechalving / recdbl_direct, and the
+    host-resident (striped) leg, each with a bitwise check on every rank."""
+    env = _env()
+    port = 29200 + os.getpid() % 500
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--nreduce", str((1 << 20) + 3), "--sweep-max", str(4 << 20)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    _used_fake(r, 2)
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["config"]["transport"] == "rccl", res["config"]
+    assert res["check"]["bitwise_mismatches_all_ranks"] == 0, res["check"]
+    for coll in res.get("adjacent_collectives", {}).get("rccl", {}).values():
+        assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]
+    assert res["host_resident"]["rccl"]["value_GiBs"] > 0, res["host_resident"]
+    for sched in ("rechalving", "recdbl_direct"):
+        assert res["schedules"]["rccl"][sched]["bitwise_mismatches_all_ranks"] == 0, res["schedules"]
+    curve = res["size_curve"]["rccl"]
+    assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
+
+
+@pytest.mark.parametrize("script", ["team_check.py", "team_mgmt_check.py"])
+def test_init_attr_multi_pe(tmp_path, script, np_=3):
+    """shmemx_init_attr across 3 processes (unique id passed out of band, no bootstrap hub):
+    RCCL barriers and the RCCL team-word agreement under the team checkers."""
+    procs = []
+    for pe in range(np_):
+        env = _env()
+        for k in ("SHMEM_PE", "SHMEM_NPES", "SHMEM_BOOTSTRAP_ADDR", "SHMEM_BOOTSTRAP_PORT"):
+            env.pop(k, None)
+        env.update({"INIT_ATTR_PE": str(pe), "INIT_ATTR_NPES": str(np_),
+                    "INIT_ATTR_UID_FILE": str(tmp_path / "uid")})
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(ROOT, "tests", "init_attr_pe.py"),
+             os.path.join(ROOT, "tools", script)],
+            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=400))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    out = "".join(o for o, _ in outs)
+    err = "".join(e for _, e in outs)
+    rcs = [p.returncode for p in procs]
+
+    class R:
+        returncode = max(rcs, key=abs)
+        stdout, stderr = out, err
+    _ok(R, np_)

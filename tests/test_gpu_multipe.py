@@ -4,7 +4,7 @@ tools/oshrun starts P PEs (P = 2, 3, 4, 8) on the box's single GPU with
 SHMEMX_TRANSPORT=p2p: each PE maps every other PE's device heap through IPC and the
 plans' transfers become direct reads of peer HBM, synchronised through node shared
 memory -- the same code that reads xGMI peer memory on the 8-GPU node.  (RCCL refuses
-two ranks on one GPU, so the RCCL transport's multi-PE runs are the 8-GPU bench's.)
+two ranks on one GPU; tests/test_gpu_fakerccl.py runs the RCCL executor's multi-PE cases.)
 """
 import os
 import re
