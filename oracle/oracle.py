@@ -48,6 +48,15 @@ def lib():
         L.oracle_fill.restype = i
         L.oracle_time_reduce_local.argtypes = [i, i, i, vp, vp, i]
         L.oracle_time_reduce_local.restype = ctypes.c_double
+        L.oracle_pe_header_bytes.argtypes = [i]
+        L.oracle_pe_header_bytes.restype = sz
+        L.oracle_pe_barrier.argtypes = [vp, i, ctypes.c_long]
+        L.oracle_pe_barrier.restype = None
+        L.oracle_pe_ring.argtypes = [vp, sz, i, i, sz, i, i, vp]
+        L.oracle_pe_ring.restype = i
+        L.oracle_pe_ring_time.argtypes = [vp, sz, i, i, sz, i, i, vp, i,
+                                          ctypes.POINTER(ctypes.c_long)]
+        L.oracle_pe_ring_time.restype = ctypes.c_double
         _L = L
     return _L
 
@@ -127,3 +136,55 @@ def bcast(srcs, root, copy_root, dsts):
 
 def time_reduce_local(op, dt, inp, inout, reps):
     return lib().oracle_time_reduce_local(op, dt, inout.size, _ptr(inp), _ptr(inout), reps)
+
+
+class PeRing:
+    """One PE of SOS's ring run by a real process (oracle_pe_ring): the N > 1 CPU
+    baseline.  Every PE process maps the same shared segment `path` (PE 0 creates it
+    before the others open it; the caller provides that ordering) holding every PE's
+    pSync words and target; the source stays private to the process."""
+
+    def __init__(self, path, P, me, count, dt, create):
+        import mmap
+        self.P, self.me, self.count, self.dt = P, me, count, dt
+        ts = lib().oracle_type_size(dt)
+        self.stride = (count * ts + 4095) & ~4095
+        self.hdr = lib().oracle_pe_header_bytes(P)
+        size = self.hdr + P * self.stride
+        fd = os.open(path, os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0), 0o600)
+        try:
+            if create:
+                os.ftruncate(fd, size)
+            self.mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        self._anchor = ctypes.c_char.from_buffer(self.mm)
+        self.base = ctypes.addressof(self._anchor)
+        self.epoch = ctypes.c_long(0)
+
+    def target(self):
+        """This PE's target as a numpy view (valid while the segment is mapped)."""
+        a = np.frombuffer(self.mm, dtype=np.uint8, count=self.count * lib().oracle_type_size(self.dt),
+                          offset=self.hdr + self.me * self.stride)
+        return a.view(NP_TYPES[self.dt])
+
+    def barrier(self):
+        self.epoch.value += 1
+        lib().oracle_pe_barrier(self.base, self.P, self.epoch.value)
+
+    def run(self, op, src):
+        rc = lib().oracle_pe_ring(self.base, self.stride, self.P, self.me, self.count, op, self.dt,
+                                  _ptr(src))
+        if rc:
+            raise ValueError(f"oracle_pe_ring rc={rc}")
+
+    def time(self, op, src, reps):
+        t = lib().oracle_pe_ring_time(self.base, self.stride, self.P, self.me, self.count, op,
+                                      self.dt, _ptr(src), reps, ctypes.byref(self.epoch))
+        if t < 0:
+            raise ValueError("oracle_pe_ring failed")
+        return t
+
+    def close(self):
+        del self._anchor
+        self.mm.close()

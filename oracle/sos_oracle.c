@@ -22,6 +22,8 @@
  *   oracle_scan          -- src/collectives.c:1111-1209 (inscan / exscan, P PEs)
  *   oracle_bcast         -- src/collectives.c:429-485 + src/collectives_c.c4:342-429
  *   oracle_*_time        -- single-core timing helpers for bench.py's cpu_baseline
+ *   oracle_pe_ring       -- src/collectives.c:647-764 as ONE PE of a real P-process job
+ *                           over a shared segment (bench.py N > 1 cpu_baseline)
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -374,4 +376,95 @@ int oracle_fill(int dt, int dist, uint64_t seed, int pe, void *dst, size_t count
         }
     }
     return 0;
+}
+
+/* ------------------------------------------------------------------------------
+ * One PE of SOS's ring (src/collectives.c:647-764) run by a real process: the CPU
+ * baseline of bench.py's N > 1 line (P single-threaded processes, one
+ * core each, shared-memory puts are memcpy as with XPMEM, src/transport_xpmem.h:95).
+ *
+ * `seg` is a MAP_SHARED segment every PE process maps, laid out as
+ *   [header: 64-B lines; line 0 = barrier counter, line 1 + 2p / 2 + 2p = PE p's
+ *    pSync[0] / pSync[1]] [PE 0 target][PE 1 target]...  (targets `stride` apart)
+ * so a PE's symmetric target and pSync sit at the same offsets in every PE's view.
+ * Put + fence + atomic add on the peer's pSync (:711-716 / :744-749) become memcpy
+ * into the peer's target, a release fence and an atomic fetch-add; SHMEM_WAIT_UNTIL
+ * (:719 / :752) spins on the PE's own pSync.  The source is the PE's private buffer
+ * (never the target, so the in-place tmp copy of :672-683 does not arise).
+ * ------------------------------------------------------------------------------ */
+#define PE_LINE 64
+
+size_t oracle_pe_header_bytes(int P)
+{
+    size_t h = (size_t) (1 + 2 * P) * PE_LINE;
+    return (h + 4095) & ~(size_t) 4095;
+}
+
+static long *pe_psync(void *seg, int pe, int k)
+{
+    return (long *) ((uint8_t *) seg + (size_t) (1 + 2 * pe + k) * PE_LINE);
+}
+
+static void pe_wait_ge(long *p, long v)
+{
+    while (__atomic_load_n(p, __ATOMIC_ACQUIRE) < v) __builtin_ia32_pause();
+}
+
+/* Sense-free barrier: the epoch-th barrier completes when the counter reaches epoch*P. */
+void oracle_pe_barrier(void *seg, int P, long epoch)
+{
+    long *c = (long *) seg;
+    __atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL);
+    pe_wait_ge(c, epoch * (long) P);
+}
+
+int oracle_pe_ring(void *seg, size_t stride, int P, int me, size_t count, int op, int dt,
+                   const void *source)
+{
+    size_t ts = oracle_type_size(dt);
+    if (!ts || me < 0 || me >= P) return -1;
+    uint8_t *base = (uint8_t *) seg + oracle_pe_header_bytes(P);
+    uint8_t *target = base + (size_t) me * stride;
+    if (count == 0) return 0;
+    if (P == 1) { memcpy(target, source, count * ts); return 0; }  /* :664-668 */
+    int peer = (me + 1) % P;
+    uint8_t *peer_target = base + (size_t) peer * stride;
+    long *my0 = pe_psync(seg, me, 0), *my1 = pe_psync(seg, me, 1);
+    long *peer0 = pe_psync(seg, peer, 0), *peer1 = pe_psync(seg, peer, 1);
+    int rc = 0;
+    for (int i = 0; i < P - 1; i++) {          /* reduce-scatter, :693-727 */
+        size_t out_n, out_d, in_n, in_d;
+        ring_chunk(count, P, (size_t) ((me - i + P) % P), ts, &out_n, &out_d);
+        ring_chunk(count, P, (size_t) ((me - i - 1 + P) % P), ts, &in_n, &in_d);
+        memcpy(peer_target + out_d, i == 0 ? (const uint8_t *) source + out_d : target + out_d,
+               out_n * ts);
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        __atomic_fetch_add(peer0, 1, __ATOMIC_RELEASE);
+        pe_wait_ge(my0, i + 1);
+        rc |= oracle_reduce_local(op, dt, (int) in_n, (const uint8_t *) source + in_d, target + in_d);
+    }
+    __atomic_store_n(my0, 0, __ATOMIC_RELEASE);     /* :730-731 */
+    for (int i = 0; i < P - 1; i++) {          /* all-gather, :737-756 */
+        size_t out_n, out_d;
+        ring_chunk(count, P, (size_t) ((me + 1 - i + P) % P), ts, &out_n, &out_d);
+        memcpy(peer_target + out_d, target + out_d, out_n * ts);
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        __atomic_fetch_add(peer1, 1, __ATOMIC_RELEASE);
+        pe_wait_ge(my1, i + 1);
+    }
+    __atomic_store_n(my1, 0, __ATOMIC_RELEASE);     /* :759-760 */
+    return rc;
+}
+
+/* `reps` ring calls, each preceded by a barrier (the team API's pSync slot reuse rule,
+ * src/shmem_team.c:540-585); barrier epochs continue from *epoch.  Returns seconds. */
+double oracle_pe_ring_time(void *seg, size_t stride, int P, int me, size_t count, int op, int dt,
+                           const void *source, int reps, long *epoch)
+{
+    double t0 = now_s();
+    for (int r = 0; r < reps; r++) {
+        oracle_pe_barrier(seg, P, ++*epoch);
+        if (oracle_pe_ring(seg, stride, P, me, count, op, dt, source)) return -1.0;
+    }
+    return now_s() - t0;
 }

@@ -135,6 +135,10 @@ def main(args, torch):
         host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank,
                            world, stream, results)
 
+    cpu_ring = {} if getattr(args, "no_cpu", False) else \
+        cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
+                          src, dst, stream)
+
     adjacent = {}
     if not getattr(args, "no_adjacent", False):
         adjacent = adjacent_collectives(args, torch, dist, L, S, dt, es, n, src, dst, stream,
@@ -206,6 +210,8 @@ def main(args, torch):
         res["host_resident"] = host_leg
     if adjacent:
         res["adjacent_collectives"] = adjacent
+    if cpu_ring:
+        res["cpu_ring_baseline"] = cpu_ring
     if rank == 0:
         print(json.dumps(res), flush=True)
     dist.barrier()
@@ -214,6 +220,90 @@ def main(args, torch):
     S.shmem_finalize()
     dist.destroy_process_group()
     return 0
+
+
+def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
+                      src, dst, stream):
+    """SOS's own CPU path beside the N > 1 line: the bench's P rank
+    processes, each pinned to one host core, run the restated ring
+    (oracle/sos_oracle.c oracle_pe_ring, src/collectives.c:647-764) over a /dev/shm
+    segment -- memcpy puts and atomic pSync adds, SOS's XPMEM model -- on the same
+    per-PE inputs at the same nreduce.  Bounded sample: one untimed call, then as many
+    calls as fit ~6 s (max over ranks).  The CPU targets are compared byte for byte with
+    the library's ring result on the GPU for the same inputs.
+    Test infrastructure in the timed-baseline role only: the product path never calls it."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    from oracle import oracle as O
+    m = args.n
+    opid = L.op_id(args.op)
+    if rank == 0:
+        log(f"[cpu ring] {world} processes x 1 core, nreduce {m}")
+    # the library's ring on the GPU for these inputs (src holds fill(seed, rank) here)
+    S.shmemx_set_reduce_algorithm(L.ALGS["ring"])
+    fn(team, dst, src, m)
+    torch.cuda.synchronize()
+    S.shmemx_set_reduce_algorithm(L.ALGS[args.alg])
+
+    allowed = sorted(os.sched_getaffinity(0))
+    stride = max(1, len(allowed) // world)
+    core = allowed[(rank * stride) % len(allowed)]
+    os.sched_setaffinity(0, {core})
+    path = f"/dev/shm/sosx_cpu_ring_{os.environ.get('MASTER_PORT', '0')}_{world}"
+    ring = None
+    try:
+        if rank == 0:
+            if os.path.exists(path):
+                os.unlink(path)
+            ring = O.PeRing(path, world, 0, m, dt, create=True)
+        dist.barrier()
+        if rank != 0:
+            ring = O.PeRing(path, world, rank, m, dt, create=False)
+        dist.barrier()
+        if rank == 0:
+            os.unlink(path)  # every PE has it mapped
+        host_src = O.fill(dt, dist_kind, seed, rank, m)
+        t_warm = ring.time(opid, host_src, 1)
+        tw = torch.tensor([t_warm], dtype=torch.float64)
+        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+        reps = max(1, min(10, int(6.0 / max(tw.item(), 1e-6))))
+        t = ring.time(opid, host_src, reps)
+        el = torch.tensor([t], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        ts = el.item() / reps
+        ring.barrier()  # every put into this PE's target has landed
+        tgt = ring.target()
+        exp = torch.from_numpy(tgt.view("u1").copy()).to("cuda")
+        del tgt
+        torch.cuda.synchronize()
+        mm = L.count_mismatch(exp.data_ptr(), dst, m, es, stream)
+        mmt = torch.tensor([mm], dtype=torch.int64)
+        dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
+        del exp, host_src
+        ring.barrier()  # nobody unmaps before every PE has read its target
+    finally:
+        if ring is not None:
+            ring.close()
+        os.sched_setaffinity(0, set(allowed))
+    cpu = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    out = {"value": round(world * m * es / ts / GiB, 3), "unit": "GiB/s", "cores": world,
+           "kind": "port", "ms_per_call": round(ts * 1e3, 3),
+           "sample": (f"SOS ring (oracle_pe_ring, src/collectives.c:647-764), "
+                      f"shmem_{args.dtype}_{args.op}_reduce nreduce={m} per PE, {world} processes "
+                      f"x 1 pinned core (every {stride}th allowed core), memcpy puts over "
+                      f"/dev/shm, {reps} timed calls after 1 warm-up, gcc -O2; host: {cpu}, "
+                      f"{len(allowed)} cores allowed"),
+           "bitwise_mismatches_vs_gpu_ring_all_ranks": int(mmt.item())}
+    if rank == 0:
+        log(f"[cpu ring] {out['ms_per_call']} ms/call, {out['value']} GiB/s whole job, "
+            f"mismatches vs GPU ring {out['bitwise_mismatches_vs_gpu_ring_all_ranks']}")
+    return out
 
 
 def host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,

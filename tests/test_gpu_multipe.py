@@ -112,6 +112,10 @@ def test_bench_team_leg(np_):
     curve = res["size_curve"]["p2p"]
     assert [r["nreduce"] for r in curve] == [1 << 20, (1 << 20) + 3, 4 << 20]
     assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
+    # SOS's ring on np_ host processes beside the line, equal to the GPU ring byte for byte
+    cpu = res["cpu_ring_baseline"]
+    assert cpu["cores"] == np_ and cpu["value"] > 0 and cpu["kind"] == "port", cpu
+    assert cpu["bitwise_mismatches_vs_gpu_ring_all_ranks"] == 0, cpu
 
 
 @pytest.mark.parametrize("np_", [3, 4])
