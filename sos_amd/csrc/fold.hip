@@ -100,6 +100,56 @@ __global__ __launch_bounds__(kThreads) void k_fold(T *out, FoldPtrs ins, Geom g)
     }
 }
 
+// Tuning variants of k_fold (bench A/B, sosx_set_fold_variant): each workgroup takes S
+// consecutive tiles (longer contiguous runs per input stream), optionally loading tile
+// j+1 before storing tile j (PF), optionally with an XCD-contiguous tile order
+// (workgroup w runs on XCD w % 8).  Same element order as k_fold.
+template <class T, class OP, int NP, int ORDER, int S, bool PF, bool XCD>
+__global__ __launch_bounds__(kThreads) void k_fold_st(T *out, FoldPtrs ins, Geom g, size_t groups)
+{
+    constexpr int V = Pack<T>::N;
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    size_t grp = blockIdx.x;
+    if (XCD && groups % 8 == 0 && grp < groups) grp = (grp % 8) * (groups / 8) + grp / 8;
+    if (grp < groups) {
+        const size_t t0 = grp * S;
+        const size_t t1 = t0 + S < g.tiles ? t0 + S : g.tiles;
+        u32x4 x[NP];
+        auto load = [&](size_t t, u32x4 (&d)[NP]) {
+            const size_t i = t * (size_t)kThreads + threadIdx.x;
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                d[k] = ldv<true>(reinterpret_cast<const u32x4 *>((const T *)ins.p[k] + g.head) + i);
+        };
+        if (PF) {
+            load(t0, x);
+            for (size_t t = t0; t < t1; ++t) {
+                u32x4 y[NP];
+                if (t + 1 < t1) load(t + 1, y);
+                stv<true>(O + t * (size_t)kThreads + threadIdx.x, fold_pack<T, OP, NP, ORDER>(x));
+#pragma unroll
+                for (int k = 0; k < NP; ++k) x[k] = y[k];
+            }
+        } else {
+            for (size_t t = t0; t < t1; ++t) {
+                load(t, x);
+                stv<true>(O + t * (size_t)kThreads + threadIdx.x, fold_pack<T, OP, NP, ORDER>(x));
+            }
+        }
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)ins.p[k])[i];
+            out[i] = fold_elem<T, OP, NP, ORDER>(v);
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
 template <class T, class OP, int NP, int ORDER>
 __global__ __launch_bounds__(kThreads) void k_fold_scalar(T *out, FoldPtrs ins,
                                                             size_t n)
@@ -238,6 +288,18 @@ int launch_fold_u(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
     return hip_ok(hipGetLastError());
 }
 
+template <class T, class OP, int NP, int ORDER, int S, bool PF, bool XCD>
+int launch_fold_st(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), 1);
+    const size_t groups = (g.tiles + S - 1) / S;
+    unsigned blocks = (unsigned)(groups + (g.has_rem ? 1 : 0));
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL((k_fold_st<T, OP, NP, ORDER, S, PF, XCD>), dim3(blocks), dim3(kThreads), 0, st,
+                       out, ins, g, groups);
+    return hip_ok(hipGetLastError());
+}
+
 template <class T, class OP, int NP, int ORDER>
 int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 {
@@ -255,6 +317,11 @@ int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
                   ORDER == SOSX_ORDER_LINEAR) {
         if (g_fold_variant == 1) return launch_fold_u<T, OP, NP, ORDER, 2>(out, ins, n, st);
         if (g_fold_variant == 2) return launch_fold_u<T, OP, NP, ORDER, 4>(out, ins, n, st);
+        if (g_fold_variant == 3) return launch_fold_st<T, OP, NP, ORDER, 4, false, false>(out, ins, n, st);
+        if (g_fold_variant == 4) return launch_fold_st<T, OP, NP, ORDER, 16, false, false>(out, ins, n, st);
+        if (g_fold_variant == 5) return launch_fold_st<T, OP, NP, ORDER, 1, false, true>(out, ins, n, st);
+        if (g_fold_variant == 6) return launch_fold_st<T, OP, NP, ORDER, 4, true, false>(out, ins, n, st);
+        if (g_fold_variant == 7) return launch_fold_st<T, OP, NP, ORDER, 16, true, true>(out, ins, n, st);
     }
     constexpr int U = NP <= 2 ? 4 : (NP <= 4 ? 2 : 1);
     Geom g = make_geom(o, n, sizeof(T), U);
@@ -355,12 +422,14 @@ int sosx_prefix(int op, int dtype, void *const *outs, const void *const *ins, in
     return dispatch<PrefixFn>(op, dtype, &pp, np, own, count, as_stream(stream));
 }
 
-// Tuning knob (bench A/B only): 0 = default, 1 = U=2, 2 = U=4 for the 8-input fp32
-// sum LINEAR fold.  Returns the previous value.
+// Tuning knob (bench A/B only) for the 8-input fp32 sum LINEAR fold: 0 = default,
+// 1 = U=2, 2 = U=4, 3/4 = 4/16 consecutive tiles per workgroup, 5 = XCD-contiguous
+// tile order, 6 = 4 tiles with the next tile's loads issued before the store,
+// 7 = 16 tiles prefetched, XCD-contiguous.  Returns the previous value.
 int sosx_set_fold_variant(int v)
 {
     const int prev = g_fold_variant;
-    if (v >= 0 && v <= 2) g_fold_variant = v;
+    if (v >= 0 && v <= 7) g_fold_variant = v;
     return prev;
 }
 

@@ -246,9 +246,19 @@ def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed
     torch.cuda.synchronize()
     S.shmemx_set_reduce_algorithm(L.ALGS[args.alg])
 
+    # one physical core per PE, consecutive (as a by-core rank binding would place them):
+    # the first hardware thread of each core in the allowed set
     allowed = sorted(os.sched_getaffinity(0))
-    stride = max(1, len(allowed) // world)
-    core = allowed[(rank * stride) % len(allowed)]
+    primaries = []
+    for c in allowed:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                first = int(f.read().replace("-", ",").split(",")[0])
+        except (OSError, ValueError):
+            first = c
+        if first == c or first not in allowed:
+            primaries.append(c)
+    core = primaries[rank % len(primaries)]
     os.sched_setaffinity(0, {core})
     path = f"/dev/shm/sosx_cpu_ring_{os.environ.get('MASTER_PORT', '0')}_{world}"
     ring = None
@@ -296,9 +306,9 @@ def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed
            "kind": "port", "ms_per_call": round(ts * 1e3, 3),
            "sample": (f"SOS ring (oracle_pe_ring, src/collectives.c:647-764), "
                       f"shmem_{args.dtype}_{args.op}_reduce nreduce={m} per PE, {world} processes "
-                      f"x 1 pinned core (every {stride}th allowed core), memcpy puts over "
-                      f"/dev/shm, {reps} timed calls after 1 warm-up, gcc -O2; host: {cpu}, "
-                      f"{len(allowed)} cores allowed"),
+                      f"x 1 pinned physical core (consecutive cores from {primaries[0]}), "
+                      f"memcpy puts over /dev/shm, {reps} timed calls after 1 warm-up, gcc -O2; "
+                      f"host: {cpu}, {len(primaries)} cores / {len(allowed)} threads allowed"),
            "bitwise_mismatches_vs_gpu_ring_all_ranks": int(mmt.item())}
     if rank == 0:
         log(f"[cpu ring] {out['ms_per_call']} ms/call, {out['value']} GiB/s whole job, "

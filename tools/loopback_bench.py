@@ -87,12 +87,13 @@ def fold_ab(a, rounds=7, reps=20):
     ins = [torch.empty(chunk * es, dtype=torch.uint8, device="cuda") for _ in range(a.P)]
     for k, b in enumerate(ins):
         L.fill(dt, 0, 0x5EED, k, b.data_ptr(), chunk)
-    outs = {v: torch.empty_like(ins[0]) for v in range(3)}
+    NV = 8
+    outs = {v: torch.empty_like(ins[0]) for v in range(NV)}
     lib = L.lib()
     ptrs = [b.data_ptr() for b in ins]
-    res = {v: [] for v in range(3)}
+    res = {v: [] for v in range(NV)}
     for _ in range(rounds):
-        for v in range(3):
+        for v in range(NV):
             lib.sosx_set_fold_variant(v)
             for _ in range(3):
                 L.fold(op, dt, L.ORDER_LINEAR, outs[v].data_ptr(), ptrs, chunk)
@@ -104,10 +105,10 @@ def fold_ab(a, rounds=7, reps=20):
             torch.cuda.synchronize()
             res[v].append(s0.elapsed_time(s1) / reps)
     lib.sosx_set_fold_variant(0)
-    same = all(torch.equal(outs[0], outs[v]) for v in (1, 2))
+    same = all(torch.equal(outs[0], outs[v]) for v in range(1, NV))
     algo = (a.P + 1) * chunk * es
     rows = {}
-    for v, name in ((0, "u1"), (1, "u2"), (2, "u4")):
+    for v, name in enumerate(("u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd")):
         ms = sorted(res[v])[len(res[v]) // 2]
         rows[name] = {"median_ms": round(ms, 5), "GBs": round(algo / (ms / 1e3) / 1e9, 1)}
     print(json.dumps({"fold_ab": rows, "P": a.P, "chunk": chunk, "bytes": algo,
