@@ -156,6 +156,21 @@ int sosx_memcpy(void *dst, const void *src, size_t bytes, void *stream);
 int sosx_gather(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,
                 void *stream);
 
+/* p2p transport signalling (internal): store wval[i] to waddr[i] (i < nw) in stream
+ * order, then wait until *qaddr[i] >= qval[i] (i < nq); a wait longer than limit_ticks
+ * of the device wall clock sets *err and gives up.  Addresses are device views of
+ * host-registered memory. */
+int sosx_p2p_signal(int nw, uint64_t *const *waddr, const uint64_t *wval, int nq,
+                    const uint64_t *const *qaddr, const uint64_t *qval, uint64_t *err,
+                    long long limit_ticks, void *stream);
+
+/* The p2p transport's signalling mode: 1 = stream-ordered device signals, 0 = host
+ * synchronisation every round (SHMEMX_P2P_SIGNAL=host), -1 = no p2p transport. */
+int sosx_p2p_signal_mode(void);
+/* Switch it between calls (1 stream, 0 host; collective: every PE at the same point of
+ * its call sequence).  Returns the previous mode, or -1 when unavailable. */
+int sosx_set_p2p_signal_mode(int mode);
+
 /* Kernel variant selection for the hot fp32/generic combine (bench/tuning only):
  * returns the previous variant.  0 = default. */
 int sosx_set_combine_variant(int variant);

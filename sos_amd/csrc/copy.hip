@@ -1,4 +1,5 @@
-// copy.hip -- multi-segment gather copy for the peer-to-peer transport.
+// copy.hip -- multi-segment gather copy and stream-ordered signalling for the
+// peer-to-peer transport.
 //
 // An allgather round pulls P-1 chunks, one from each peer's HBM over its own xGMI
 // link.  One launch copies all segments at once (workgroups dealt across segments in
@@ -40,6 +41,45 @@ __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g)
             const uint64_t tail0 = g.head[t] + g.nvec[t] * 16;
             for (uint64_t b = tail0 + threadIdx.x; b < g.bytes[t]; b += kThreads)
                 g.dst[t][b] = g.src[t][b];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Stream-ordered signalling of the peer-to-peer transport (p2p.cpp): one lane per
+// counter.  Lanes first store their new counter values (monotonic transfer counters in
+// node shared memory, registered with HIP so the GPU reaches them), then every lane
+// waits until its counter reaches its wanted value.  Because the launch sits in stream
+// order, the stores happen after the kernels that produced the sent bytes and the
+// waits hold back the kernels that read a peer's bytes.  Every wait is bounded by
+// `limit` wall-clock ticks: on expiry the lane sets *err and returns, so the grid
+// always drains (the host turns *err into an error after the stream synchronises).
+// ---------------------------------------------------------------------------------
+constexpr int kMaxSig = 64;
+
+struct SigArgs {
+    uint64_t *waddr[kMaxSig];
+    uint64_t wval[kMaxSig];
+    const uint64_t *qaddr[kMaxSig];
+    uint64_t qval[kMaxSig];
+    uint64_t *err;
+    long long limit;
+    int nw, nq;
+};
+
+__global__ __launch_bounds__(kMaxSig) void k_p2p_signal(SigArgs a)
+{
+    const int i = threadIdx.x;
+    if (i < a.nw) __hip_atomic_store(a.waddr[i], a.wval[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (i < a.nq) {
+        const long long t0 = wall_clock64();
+        while (__hip_atomic_load(a.qaddr[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.qval[i]) {
+            if (wall_clock64() - t0 > a.limit) {
+                __hip_atomic_store(a.err, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
         }
     }
 }
@@ -87,6 +127,38 @@ int sosx_gather(int nseg, const void *const *srcs, void *const *dsts, const size
         if (blocks < 1) blocks = 1;
         if (blocks > 16384) blocks = 16384;
         hipLaunchKernelGGL(k_gather, dim3((unsigned)blocks), dim3(kThreads), 0, st, g);
+        if (hipGetLastError() != hipSuccess) return SOSX_ERR_HIP;
+    }
+    return SOSX_OK;
+}
+
+// One signalling step of the p2p transport on `stream`: store vals[i] to waddr[i]
+// (i < nw), then wait until *qaddr[i] >= qval[i] (i < nq), each wait bounded by
+// `limit_ticks` of the device wall clock (expiry sets *err).  All addresses are device
+// views of host-registered memory.  More than 64 entries run as several launches,
+// every store launch before the first wait launch.
+int sosx_p2p_signal(int nw, uint64_t *const *waddr, const uint64_t *wval, int nq,
+                    const uint64_t *const *qaddr, const uint64_t *qval, uint64_t *err,
+                    long long limit_ticks, void *stream)
+{
+    if (nw < 0 || nq < 0 || (nq && !err)) return SOSX_ERR_ARG;
+    hipStream_t st = as_stream(stream);
+    int w = 0, q = 0;
+    while (w < nw || q < nq) {
+        SigArgs a;
+        memset(&a, 0, sizeof(a));
+        a.err = err;
+        a.limit = limit_ticks;
+        while (w < nw && a.nw < kMaxSig) {
+            a.waddr[a.nw] = waddr[w];
+            a.wval[a.nw++] = wval[w++];
+        }
+        if (w == nw)  // waits only once every store has been issued
+            while (q < nq && a.nq < kMaxSig) {
+                a.qaddr[a.nq] = qaddr[q];
+                a.qval[a.nq++] = qval[q++];
+            }
+        hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(kMaxSig), 0, st, a);
         if (hipGetLastError() != hipSuccess) return SOSX_ERR_HIP;
     }
     return SOSX_OK;

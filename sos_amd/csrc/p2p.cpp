@@ -23,6 +23,16 @@
 // For the SOS ring plan this is: fold chunk `me` straight from the P-1 peers' sources
 // over their xGMI links (P+1 HBM/xGMI streams, one launch), then gather the P-1 owned
 // chunks -- the RCCL version's scratch round trip disappears.
+//
+// Two signalling modes, agreed by every PE when the heap is mapped:
+//   stream (default): the counters move in stream order, written and awaited by a
+//     one-workgroup kernel (sosx_p2p_signal) on host-registered node shared memory.  A
+//     call enqueues all of its rounds at once -- signal, folds/gathers, signal, ... --
+//     and the host synchronises once, at the end.  Each PE's buffer offsets for the
+//     call travel ahead of the data through a small descriptor ring per ordered pair
+//     (host handshake only, never waiting on a GPU).
+//   host (SHMEMX_P2P_SIGNAL=host, or HIP cannot register the segment): the host
+//     synchronises the stream and moves the counters itself every round, as steps 1-4.
 #include <time.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -30,6 +40,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <functional>
 #include <map>
 #include <tuple>
 #include <vector>
@@ -51,9 +62,24 @@ namespace {
 
 constexpr int kMaxPE = 64;
 
+constexpr int kDescRing = 4;
+
+// Per-call buffer offsets of a sender, as the receiver needs them to find its bytes.
+struct Desc {
+    uint64_t src_off, dst_off, scr_off, mis;
+};
+
 struct P2PShared {
     std::atomic<uint64_t> posted[kMaxPE][kMaxPE];
     std::atomic<uint64_t> consumed[kMaxPE][kMaxPE];
+    // stream mode: counters stored by the GPUs (sosx_p2p_signal), cumulative per pair
+    uint64_t dposted[kMaxPE][kMaxPE];
+    uint64_t dconsumed[kMaxPE][kMaxPE];
+    uint64_t sig_err[kMaxPE];                  // a PE's timed-out device wait
+    // stream mode: descriptor ring per ordered pair [from][to]
+    Desc desc[kMaxPE][kMaxPE][kDescRing];
+    std::atomic<uint64_t> desc_posted[kMaxPE][kMaxPE];
+    std::atomic<uint64_t> desc_read[kMaxPE][kMaxPE];
     struct Pub {
         std::atomic<uint64_t> src_off, dst_off, scr_off, mis;
     } pub[kMaxPE];
@@ -70,9 +96,27 @@ struct Local {
 
 Local g_local;
 
+// stream-mode signalling state
+struct Sig {
+    bool on = false;                // stream mode in use
+    bool capable = false;           // every PE registered the segment (agreed)
+    bool registered = false;
+    char *dbase = nullptr;          // device view of the shared segment
+    long long limit_ticks = 0;      // device wall-clock ticks of SHMEMX_P2P_TIMEOUT
+    uint64_t posted[kMaxPE] = {0};  // my sends to each world PE (cumulative)
+    uint64_t seen[kMaxPE] = {0};    // sends from each world PE I have waited for
+    uint64_t desc_sent[kMaxPE] = {0}, desc_got[kMaxPE] = {0};
+};
+Sig g_sig;
+
 P2PShared *shared()
 {
     return (P2PShared *)st().shm.extra;
+}
+
+template <class X> X *dev(X *host)
+{
+    return (X *)(g_sig.dbase + ((char *)host - (char *)shared()));
 }
 
 // Wall-clock bound of one wait (SHMEMX_P2P_TIMEOUT seconds, default 300): a peer that
@@ -177,12 +221,337 @@ uint64_t team_word_get(int which, int world_pe)
     return shared()->team_word[which][world_pe].load(std::memory_order_acquire);
 }
 
+namespace {
+
+// One round's local ops (copies, zero fills, folds, prefixes); fold/prefix inputs come
+// from `ins` (received chunks may point into peer memory).
+int run_round_ops(const sosplan::Round &r, const std::vector<std::vector<const void *>> &ins,
+                  const std::function<char *(int, uint64_t)> &local_ptr, int op, int dt,
+                  hipStream_t stream)
+{
+    for (size_t i = 0; i < r.ops.size(); ++i) {
+        const auto &l = r.ops[i];
+        if (l.kind == sosplan::COPY) {
+            if (ins[i][0] != local_ptr(l.out_buf, l.out_off) &&
+                hipMemcpyAsync(local_ptr(l.out_buf, l.out_off), ins[i][0], l.count,
+                               hipMemcpyDeviceToDevice, stream) != hipSuccess)
+                return SOSX_ERR_HIP;
+            continue;
+        }
+        if (l.kind == sosplan::ZERO) {
+            if (hipMemsetAsync(local_ptr(l.out_buf, l.out_off), 0, l.count, stream) != hipSuccess)
+                return SOSX_ERR_HIP;
+            continue;
+        }
+        if (l.kind == sosplan::PREFIX) {
+            void *outs[sosplan::PLAN_MAX_PE];
+            for (int k = 0; k < l.nout; ++k) outs[k] = local_ptr(l.outs_buf[k], l.outs_off[k]);
+            prof_mark(0, false, stream);
+            int rc = sosx_prefix(op, dt, outs, ins[i].data(), l.nin, l.own, l.count, stream);
+            prof_mark(0, true, stream);
+            if (rc) return rc;
+            continue;
+        }
+        prof_mark(0, false, stream);
+        int rc = sosx_fold(op, dt, l.order, local_ptr(l.out_buf, l.out_off), ins[i].data(), l.nin,
+                           l.count, stream);
+        prof_mark(0, true, stream);
+        if (rc) return rc;
+    }
+    return SOSX_OK;
+}
+
+// Does any output of the round's ops overlap bytes this PE sends in the same round?
+// If not, folds/prefixes may read received chunks in place (the peers' memory) before
+// the round's sends are consumed.
+bool round_fusable(const sosplan::Round &r, uint64_t ts,
+                   const std::function<char *(int, uint64_t)> &local_ptr)
+{
+    for (const auto &l : r.ops) {
+        const bool typed = l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX;
+        const uint64_t ob = typed ? l.count * ts : l.count;
+        const int nout = l.kind == sosplan::PREFIX ? l.nout : 1;
+        for (int k = 0; k < nout; ++k) {
+            const char *o = l.kind == sosplan::PREFIX ? local_ptr(l.outs_buf[k], l.outs_off[k])
+                                                      : local_ptr(l.out_buf, l.out_off);
+            for (const auto &x : r.xfers)
+                if (x.send && overlaps(o, ob, local_ptr(x.buf, x.off), x.bytes)) return false;
+        }
+    }
+    return true;
+}
+
+// Stream-mode executor: the whole call is enqueued at once (see the header).
+int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count,
+                    uint64_t ts, const P2PBufs &b, int op, int dt, hipStream_t stream)
+{
+    State &s = st();
+    P2PShared *sh = shared();
+    const int me = t.my_idx;
+    const int my_world = t.world_rank(me);
+    const bool tr = trace_on();
+    double tp = tr ? now_s() : 0;
+    auto phase = [&](int ph) {
+        if (!tr) return;
+        const double now = now_s();
+        g_trace.t[ph] += now - tp;
+        tp = now;
+    };
+    std::function<char *(int, uint64_t)> local_ptr = [&](int buf, uint64_t off) -> char * {
+        return (buf == sosplan::SRC ? (char *)b.src : buf == sosplan::DST ? b.dst : b.scr) + off;
+    };
+    // 1. descriptors: publish this call's offsets to every PE this call sends to, then
+    //    read those of every PE it receives from (host handshake, no GPU wait)
+    std::vector<char> sends_to((size_t)t.size, 0), recvs_from((size_t)t.size, 0);
+    for (const auto &r : plan.rounds)
+        for (const auto &x : r.xfers) (x.send ? sends_to : recvs_from)[(size_t)x.peer] = 1;
+    const Desc mine{b.src_off, b.dst_off, b.scr_off,
+                    (uint64_t)(b.smis & 15) | (uint64_t)(b.dmis & 15) << 4};
+    for (int q = 0; q < t.size; ++q) {
+        if (!sends_to[(size_t)q]) continue;
+        const int pw = t.world_rank(q);
+        const uint64_t idx = g_sig.desc_sent[pw]++;
+        if (idx >= (uint64_t)kDescRing)
+            spin_until(sh->desc_read[my_world][pw], idx + 1 - kDescRing, "a peer to take a descriptor");
+        sh->desc[my_world][pw][idx % kDescRing] = mine;
+        sh->desc_posted[my_world][pw].store(idx + 1, std::memory_order_release);
+    }
+    std::vector<Desc> peer_desc((size_t)t.size);
+    for (int q = 0; q < t.size; ++q) {
+        if (!recvs_from[(size_t)q]) continue;
+        const int pw = t.world_rank(q);
+        const uint64_t idx = g_sig.desc_got[pw]++;
+        spin_until(sh->desc_posted[pw][my_world], idx + 1, "a peer's call descriptor");
+        peer_desc[(size_t)q] = sh->desc[pw][my_world][idx % kDescRing];
+        sh->desc_read[pw][my_world].store(idx + 1, std::memory_order_release);
+    }
+    phase(PH_WAIT_POST);
+    // pending signalling step: stores first, then waits (merged across a round boundary
+    // when no local op sits between them)
+    std::map<uint64_t *, uint64_t> pw_store;
+    std::map<const uint64_t *, uint64_t> pw_wait;
+    auto flush = [&]() -> int {
+        if (pw_store.empty() && pw_wait.empty()) return SOSX_OK;
+        std::vector<uint64_t *> wa;
+        std::vector<uint64_t> wv;
+        std::vector<const uint64_t *> qa;
+        std::vector<uint64_t> qv;
+        for (auto &kv : pw_store) {
+            wa.push_back(dev(kv.first));
+            wv.push_back(kv.second);
+        }
+        for (auto &kv : pw_wait) {
+            qa.push_back(dev(kv.first));
+            qv.push_back(kv.second);
+        }
+        pw_store.clear();
+        pw_wait.clear();
+        return sosx_p2p_signal((int)wa.size(), wa.data(), wv.data(), (int)qa.size(), qa.data(),
+                               qv.data(), dev(&sh->sig_err[my_world]), g_sig.limit_ticks, stream);
+    };
+    std::vector<int> recv_idx((size_t)t.size, 0);  // k-th receive from each team peer
+    for (const auto &r : plan.rounds) {
+        if (r.xfers.empty()) {
+            int rc = flush();
+            if (rc) return rc;
+            std::vector<std::vector<const void *>> ins(r.ops.size());
+            for (size_t i = 0; i < r.ops.size(); ++i)
+                for (int k = 0; k < r.ops[i].nin; ++k)
+                    ins[i].push_back(local_ptr(r.ops[i].in_buf[k], r.ops[i].in_off[k]));
+            rc = run_round_ops(r, ins, local_ptr, op, dt, stream);
+            if (rc) return rc;
+            continue;
+        }
+        // post this round's sends (their bytes are final in stream order), wait for the
+        // peers' posts of what this round receives
+        for (const auto &x : r.xfers) {
+            const int pw = t.world_rank(x.peer);
+            if (x.send) {
+                pw_store[&sh->dposted[my_world][pw]] = ++g_sig.posted[pw];
+            } else {
+                pw_wait[&sh->dposted[pw][my_world]] = ++g_sig.seen[pw];
+            }
+        }
+        int rc = flush();
+        if (rc) return rc;
+        struct Seg { const char *src; char *dst; uint64_t bytes; bool used; };
+        std::vector<Seg> segs;
+        for (const auto &x : r.xfers) {
+            if (x.send) continue;
+            const int pw = t.world_rank(x.peer);
+            const Desc &d = peer_desc[(size_t)x.peer];
+            const auto &sends = peer_sends(alg, t.size, x.peer, me, count, ts, d.mis);
+            const int k = recv_idx[(size_t)x.peer]++;
+            if (k >= (int)sends.size() || sends[(size_t)k].bytes != x.bytes)
+                raise_error("p2p transport: plan mismatch with PE %d", pw);
+            const PeerSend &ps = sends[(size_t)k];
+            const uint64_t boff = ps.buf == sosplan::SRC ? d.src_off
+                                : ps.buf == sosplan::DST ? d.dst_off : d.scr_off;
+            segs.push_back(Seg{s.peer_heap[(size_t)pw] + boff + ps.off, local_ptr(x.buf, x.off),
+                               x.bytes, false});
+        }
+        const bool fuse_ok = round_fusable(r, ts, local_ptr);
+        std::vector<std::vector<const void *>> ins(r.ops.size());
+        for (size_t i = 0; i < r.ops.size(); ++i) {
+            const auto &l = r.ops[i];
+            for (int k = 0; k < l.nin; ++k) {
+                const char *p = local_ptr(l.in_buf[k], l.in_off[k]);
+                if (fuse_ok && (l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX))
+                    for (auto &sg : segs)
+                        if (sg.dst == p && sg.bytes == l.count * ts) {
+                            p = sg.src;
+                            sg.used = true;
+                        }
+                ins[i].push_back(p);
+            }
+        }
+        std::vector<const void *> gs;
+        std::vector<void *> gd;
+        std::vector<size_t> gb;
+        for (auto &sg : segs)
+            if (!sg.used) {
+                gs.push_back(sg.src);
+                gd.push_back(sg.dst);
+                gb.push_back(sg.bytes);
+            }
+        if (!gs.empty()) {
+            prof_mark(1, false, stream);
+            rc = sosx_gather((int)gs.size(), gs.data(), gd.data(), gb.data(), stream);
+            prof_mark(1, true, stream);
+            if (rc) return rc;
+        }
+        if (fuse_ok) {
+            rc = run_round_ops(r, ins, local_ptr, op, dt, stream);
+            if (rc) return rc;
+        }
+        // this round's receives are read: mark them consumed; this PE's sends must be
+        // consumed before anything overwrites them (the next round's ops or the caller)
+        for (const auto &x : r.xfers) {
+            const int pw = t.world_rank(x.peer);
+            if (x.send) pw_wait[&sh->dconsumed[my_world][pw]] = g_sig.posted[pw];
+            else pw_store[&sh->dconsumed[pw][my_world]] = g_sig.seen[pw];
+        }
+        if (!fuse_ok) {
+            rc = flush();
+            if (rc) return rc;
+            rc = run_round_ops(r, ins, local_ptr, op, dt, stream);
+            if (rc) return rc;
+        }
+    }
+    int rc = flush();
+    if (rc) return rc;
+    phase(PH_ENQUEUE);
+    const hipError_t e = hipStreamSynchronize(stream);
+    phase(PH_SYNC_END);
+    if (__atomic_load_n(&sh->sig_err[my_world], __ATOMIC_ACQUIRE))
+        raise_error("p2p transport: timed out after %.0f s waiting for a peer (device wait)",
+                    wait_limit_s());
+    if (tr && ++g_trace.calls % g_trace.every == 0) {
+        const double k = 1e6 / (double)g_trace.every;
+        fprintf(stderr, "[%04d] p2p trace, stream mode (calls %ld-%ld, us/call): descriptors %.1f "
+                "enqueue %.1f sync-end %.1f\n", s.my_pe, g_trace.calls - g_trace.every + 1,
+                g_trace.calls, g_trace.t[PH_WAIT_POST] * k, g_trace.t[PH_ENQUEUE] * k,
+                g_trace.t[PH_SYNC_END] * k);
+        for (double &v : g_trace.t) v = 0;
+    }
+    return e == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
+}
+
+}  // namespace
+
+// Signalling setup (runtime.cpp ensure_device_heap, collective): register the shared
+// segment with HIP on every PE and agree through the bootstrap whether stream mode is
+// possible everywhere.  The mode in use starts as SHMEMX_P2P_SIGNAL (host by default:
+// on one GPU shared by 2 or 8 PE processes the host mode measured faster, profiles/
+// r2_p2p_signal_latency.txt) and can be switched collectively (sosx_set_p2p_signal_mode).
+void p2p_signal_setup()
+{
+    State &s = st();
+    // a fresh (zero-filled) segment: every pair's counters restart from 0 here too
+    const bool reg = g_sig.registered;
+    g_sig = Sig();
+    g_sig.registered = reg;
+    g_local = Local();
+    if (!s.shm.extra || s.n_pes <= 1) return;
+    int ok = 1;
+    void *dptr = nullptr;
+    if (!g_sig.registered) {
+        const size_t bytes = (sizeof(P2PShared) + 4095) & ~(size_t)4095;
+        hipError_t he = hipHostRegister(s.shm.extra, bytes, hipHostRegisterMapped);
+        if (he == hipSuccess) g_sig.registered = true;
+        else {
+            (void)hipGetLastError();
+            debug_msg("p2p: hipHostRegister of the shared segment failed (%s)", hipGetErrorString(he));
+        }
+    }
+    if (g_sig.registered) {
+        ok = hipHostGetDevicePointer(&dptr, s.shm.extra, 0) == hipSuccess && dptr;
+        if (!ok) (void)hipGetLastError();
+    } else {
+        ok = 0;
+    }
+    int rate_khz = 0;
+    if (ok && (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, s.device) != hipSuccess ||
+               rate_khz <= 0)) {
+        (void)hipGetLastError();
+        ok = 0;
+    }
+    std::vector<int> oks((size_t)s.n_pes);
+    if (sosboot::hub_allgather(&s.hub, &ok, sizeof(ok), oks.data()) != 0)
+        raise_error("p2p: signalling mode agreement failed");
+    for (int v : oks) ok &= v;
+    g_sig.capable = ok != 0;
+    g_sig.dbase = (char *)dptr;
+    g_sig.limit_ticks = (long long)(wait_limit_s() * 1e3 * (double)rate_khz);
+    const char *e = getenv("SHMEMX_P2P_SIGNAL");  // the same on every PE (job environment)
+    g_sig.on = g_sig.capable && e && strcmp(e, "stream") == 0;
+    debug_msg("p2p transport signalling: %s (stream mode %s)", g_sig.on ? "stream" : "host",
+              g_sig.capable ? "available" : "unavailable");
+}
+
+void p2p_signal_teardown()
+{
+    if (g_sig.registered && st().shm.extra) (void)hipHostUnregister(st().shm.extra);
+    g_sig.registered = false;
+    g_sig.on = false;
+}
+
+bool p2p_stream_signalling() { return g_sig.on; }
+bool p2p_stream_capable() { return g_sig.capable; }
+void p2p_set_stream_signalling(bool on) { g_sig.on = on && g_sig.capable; }
+
+}  // namespace sosrt
+
+// 1 = stream-ordered device signals, 0 = host synchronisation, -1 = no p2p transport
+extern "C" int sosx_p2p_signal_mode(void)
+{
+    const sosrt::State &s = sosrt::st();
+    if (!s.p2p_ready || s.n_pes <= 1) return -1;
+    return sosrt::p2p_stream_signalling() ? 1 : 0;
+}
+
+// Switch the p2p signalling mode (1 stream, 0 host) between calls; collective: every PE
+// switches at the same point of its call sequence.  Returns the previous mode, or -1
+// (nothing changed) when the mode is unavailable.
+extern "C" int sosx_set_p2p_signal_mode(int mode)
+{
+    const sosrt::State &s = sosrt::st();
+    if (!s.p2p_ready || s.n_pes <= 1 || mode < 0 || mode > 1) return -1;
+    if (mode == 1 && !sosrt::p2p_stream_capable()) return -1;
+    const int prev = sosrt::p2p_stream_signalling() ? 1 : 0;
+    sosrt::p2p_set_stream_signalling(mode == 1);
+    return prev;
+}
+
+namespace sosrt {
+
 int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, uint64_t ts,
              const P2PBufs &b, int op, int dt, hipStream_t stream)
 {
     State &s = st();
     P2PShared *sh = shared();
     if (!sh) return SOSX_ERR_STATE;
+    if (g_sig.on) return p2p_exec_stream(plan, t, alg, count, ts, b, op, dt, stream);
     const int me = t.my_idx;
     const int my_world = t.world_rank(me);
     sh->pub[my_world].src_off.store(b.src_off, std::memory_order_relaxed);
@@ -199,7 +568,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
         g_trace.t[ph] += now - tp;
         tp = now;
     };
-    auto local_ptr = [&](int buf, uint64_t off) -> char * {
+    std::function<char *(int, uint64_t)> local_ptr = [&](int buf, uint64_t off) -> char * {
         return (buf == sosplan::SRC ? (char *)b.src : buf == sosplan::DST ? b.dst : b.scr) + off;
     };
     for (const auto &r : plan.rounds) {
@@ -239,18 +608,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
             segs.push_back(Seg{remote, local_ptr(x.buf, x.off), x.bytes, pw, false});
         }
         // 3. folds/prefixes read received chunks in place when no output overlaps a send
-        bool fuse_ok = true;
-        for (const auto &l : r.ops) {
-            const bool typed = l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX;
-            const uint64_t ob = typed ? l.count * ts : l.count;
-            const int nout = l.kind == sosplan::PREFIX ? l.nout : 1;
-            for (int k = 0; k < nout; ++k) {
-                const char *o = l.kind == sosplan::PREFIX ? local_ptr(l.outs_buf[k], l.outs_off[k])
-                                                          : local_ptr(l.out_buf, l.out_off);
-                for (const auto &x : r.xfers)
-                    if (x.send && overlaps(o, ob, local_ptr(x.buf, x.off), x.bytes)) fuse_ok = false;
-            }
-        }
+        const bool fuse_ok = round_fusable(r, ts, local_ptr);
         std::vector<std::vector<const void *>> fold_ins(r.ops.size());
         for (size_t i = 0; i < r.ops.size(); ++i) {
             const auto &l = r.ops[i];
@@ -280,38 +638,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
             prof_mark(1, true, stream);
             if (rc) return rc;
         }
-        auto run_ops = [&]() -> int {
-            for (size_t i = 0; i < r.ops.size(); ++i) {
-                const auto &l = r.ops[i];
-                if (l.kind == sosplan::COPY) {
-                    if (fold_ins[i][0] != local_ptr(l.out_buf, l.out_off) &&
-                        hipMemcpyAsync(local_ptr(l.out_buf, l.out_off), fold_ins[i][0], l.count,
-                                       hipMemcpyDeviceToDevice, stream) != hipSuccess)
-                        return SOSX_ERR_HIP;
-                    continue;
-                }
-                if (l.kind == sosplan::ZERO) {
-                    if (hipMemsetAsync(local_ptr(l.out_buf, l.out_off), 0, l.count, stream) != hipSuccess)
-                        return SOSX_ERR_HIP;
-                    continue;
-                }
-                if (l.kind == sosplan::PREFIX) {
-                    void *outs[sosplan::PLAN_MAX_PE];
-                    for (int k = 0; k < l.nout; ++k) outs[k] = local_ptr(l.outs_buf[k], l.outs_off[k]);
-                    prof_mark(0, false, stream);
-                    int rc = sosx_prefix(op, dt, outs, fold_ins[i].data(), l.nin, l.own, l.count, stream);
-                    prof_mark(0, true, stream);
-                    if (rc) return rc;
-                    continue;
-                }
-                prof_mark(0, false, stream);
-                int rc = sosx_fold(op, dt, l.order, local_ptr(l.out_buf, l.out_off),
-                                   fold_ins[i].data(), l.nin, l.count, stream);
-                prof_mark(0, true, stream);
-                if (rc) return rc;
-            }
-            return SOSX_OK;
-        };
+        auto run_ops = [&]() { return run_round_ops(r, fold_ins, local_ptr, op, dt, stream); };
         if (fuse_ok) {
             int rc = run_ops();
             if (rc) return rc;

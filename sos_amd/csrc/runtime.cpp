@@ -321,6 +321,7 @@ void ensure_device_heap()
     s.p2p_ready = true;
     debug_msg("device heap %zu B (stage %zu B) mapped on %d PEs", s.dev_heap_bytes,
               s.sym_stage_bytes, s.n_pes);
+    p2p_signal_setup();
 }
 
 // ---------------------------------------------------------------------------------
@@ -619,6 +620,7 @@ void shmem_finalize(void)
     s.sym_stage = nullptr;
     s.host_heap = Heap();
     s.dev_heap = Heap();
+    p2p_signal_teardown();
     s.shm.detach();
     sosboot::hub_close(&s.hub);
     for (auto &kv : s.dev_allocs) (void)hipFree(kv.first);

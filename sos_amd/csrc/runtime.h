@@ -157,6 +157,13 @@ void ensure_device_heap();
 size_t p2p_shared_bytes();
 void team_word_put(int which, int world_pe, uint64_t v);   // node shm (p2p.cpp)
 uint64_t team_word_get(int which, int world_pe);
+// p2p signalling mode (p2p.cpp): stream-ordered device signals on the registered shm
+// segment, or host synchronisation every round.  setup is collective.
+void p2p_signal_setup();
+void p2p_signal_teardown();
+bool p2p_stream_signalling();
+bool p2p_stream_capable();
+void p2p_set_stream_signalling(bool on);
 
 }  // namespace sosrt
 

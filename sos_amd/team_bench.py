@@ -7,9 +7,11 @@ is libsos_amd.so behind the public C API: shmem_init() bootstraps over TCP
 (shmemx_malloc_device), and every step is one shmem_<T>_<op>_reduce(SHMEM_TEAM_WORLD).
 
 Both inter-PE transports are measured (SHMEMX_TRANSPORT=both):
-  rccl : ncclSend/ncclRecv over xGMI + the HIP fold kernels (the library default;
-         `value` is this one)
-  p2p  : the fold kernel reads the peers' chunks straight out of their IPC-mapped HBM.
+  rccl       : ncclSend/ncclRecv over xGMI + the HIP fold kernels (the library default)
+  p2p        : the fold kernel reads the peers' chunks straight out of their IPC-mapped
+               HBM; the host moves the transfer counters every round
+  p2p_stream : the same with stream-ordered device signals (one host sync per call)
+`value` is the fastest one whose bitwise check is clean.
 Self-check: after timing, every rank regenerates all P inputs on its own GPU and
 re-evaluates the schedule's element order with the fold kernel (ring: chunk c folded
 from PE c rightwards, src/collectives.c:693-727; tree schedules: the recdbl_sw tree),
@@ -27,6 +29,26 @@ GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0
 XGMI_LINK_GBS = 153.0   # per link, per direction, nominal
 XGMI_LINKS = 7
+
+
+# Measured transports: (name, shmemx_set_transport id, p2p signalling mode).  p2p runs
+# twice: counters moved by the host every round (the default) and by stream-ordered
+# device signals (sosx_set_p2p_signal_mode(1)); every leg reports each one.
+TRANSPORTS = (("rccl", 0, None), ("p2p", 1, 0), ("p2p_stream", 1, 1))
+T_NAMES = tuple(t[0] for t in TRANSPORTS)
+
+
+def use_transport(S, L, tname):
+    """Switch every PE (collectively) to `tname`; False when it is unavailable."""
+    _, tid, sig = next(t for t in TRANSPORTS if t[0] == tname)
+    if S.lib().shmemx_set_transport(tid) < 0:
+        return False
+    return sig is None or L.lib().sosx_set_p2p_signal_mode(sig) >= 0
+
+
+def reset_transport(S, L):
+    S.lib().shmemx_set_transport(0)
+    L.lib().sosx_set_p2p_signal_mode(0)
 
 
 def log(*a):
@@ -83,8 +105,8 @@ def main(args, torch):
     results = {}
     if rank == 0:
         log(f"[team] {world} PEs, nreduce {n}, alg {name}: heap {os.environ['SHMEMX_DEVICE_HEAP_SIZE']} B")
-    for tname, tid in (("rccl", 0), ("p2p", 1)):
-        if S.lib().shmemx_set_transport(tid) < 0:
+    for tid, tname in enumerate(T_NAMES):
+        if not use_transport(S, L, tname):
             results[tname] = {"available": False}
             continue
         if rank == 0:
@@ -146,7 +168,7 @@ def main(args, torch):
 
     # `value` is the faster transport among those whose bitwise check is clean (both are
     # the library's: SHMEMX_TRANSPORT=rccl|p2p); every measured transport is reported
-    measured = [k for k in ("rccl", "p2p") if results[k].get("available", True)]
+    measured = [k for k in T_NAMES if results[k].get("available", True)]
     clean = [k for k in measured if results[k]["mismatches"] == 0]
     primary = min(clean or measured, key=lambda k: results[k]["t_step"])
     r = results[primary]
@@ -185,7 +207,8 @@ def main(args, torch):
         "config": {"workload": f"shmem_{args.dtype}_{args.op}_reduce(SHMEM_TEAM_WORLD) nreduce={n} "
                                f"per PE, {world} PEs (1 per MI355X), "
                                + ("RCCL over xGMI + HIP fold" if primary == "rccl" else
-                                  "p2p reads of IPC-mapped peer HBM + HIP fold"),
+                                  "p2p reads of IPC-mapped peer HBM + HIP fold"
+                                  + (", stream-ordered signals" if primary == "p2p_stream" else "")),
                    "nreduce": n, "algorithm": name, "transport": primary,
                    "parallelism": f"pe{world}"},
         "roofline": {"bound": "hbm", "kernel": "sos::k_fold (fused P-way combine)",
@@ -201,7 +224,8 @@ def main(args, torch):
     res["transports"] = {k: team_roof(results[k]) for k in measured}
     res["transport_choice"] = ("value = the faster of the measured transports with a clean "
                                "bitwise check; the library default is rccl "
-                               "(SHMEMX_TRANSPORT selects)")
+                               "(SHMEMX_TRANSPORT selects; p2p_stream = p2p with "
+                               "SHMEMX_P2P_SIGNAL=stream)")
     if curve:
         res["size_curve"] = curve
     if schedules:
@@ -335,8 +359,8 @@ def host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, see
     host = np.ctypeslib.as_array((ctypes_u8 * nbytes).from_address(hsrc))
     host[:] = tmp.cpu().numpy()
     out = {"nreduce": m, "buffers": "shmem_malloc (pinned host symmetric heap)"}
-    for tname, tid in (("rccl", 0), ("p2p", 1)):
-        if not headline.get(tname, {}).get("available", True) or S.lib().shmemx_set_transport(tid) < 0:
+    for tid, tname in enumerate(T_NAMES):
+        if not headline.get(tname, {}).get("available", True) or not use_transport(S, L, tname):
             continue
         reps = max(3, min(args.steps, 10))
         fn(team, hdst, hsrc, m)
@@ -353,7 +377,7 @@ def host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, see
                       "payload_GiBs_per_pe": round(nbytes / ts / GiB, 3),
                       "pcie_bytes_per_pe": 2 * nbytes}
         log(f"[host resident] {tname} n={m} {out[tname]['ms_per_call']} ms/call")
-    S.lib().shmemx_set_transport(0)
+    reset_transport(S, L)
     S.lib().shmem_free(hdst)
     S.lib().shmem_free(hsrc)
     return out
@@ -368,8 +392,8 @@ def size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank,
     P = world
     out = {}
     alg = L.ALGS[args.alg]
-    for tname, tid in (("rccl", 0), ("p2p", 1)):
-        if not headline.get(tname, {}).get("available", True) or S.lib().shmemx_set_transport(tid) < 0:
+    for tid, tname in enumerate(T_NAMES):
+        if not headline.get(tname, {}).get("available", True) or not use_transport(S, L, tname):
             continue
         rows = []
         for m in sizes:
@@ -412,7 +436,7 @@ def size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank,
             log(f"[team curve] {tname} n={m} {row['ms_per_call']} ms/call {row['value_GiBs']} GiB/s "
                 f"busbw {row['busbw_GBs']} GB/s")
         out[tname] = rows
-    S.lib().shmemx_set_transport(0)
+    reset_transport(S, L)
     return out
 
 
@@ -425,8 +449,8 @@ def other_schedules(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, 
     n, P = args.n, world
     out = {}
     steps = max(3, min(args.steps, 10))
-    for tname, tid in (("rccl", 0), ("p2p", 1)):
-        if not headline.get(tname, {}).get("available", True) or S.lib().shmemx_set_transport(tid) < 0:
+    for tid, tname in enumerate(T_NAMES):
+        if not headline.get(tname, {}).get("available", True) or not use_transport(S, L, tname):
             continue
         for sname in ("rechalving", "recdbl_direct"):
             alg = L.ALGS[sname]
@@ -463,7 +487,7 @@ def other_schedules(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, 
                 "busbw_GBs": round(wire / ts / 1e9, 1),
                 "bitwise_mismatches_all_ranks": int(mmt.item())}
     S.shmemx_set_reduce_algorithm(L.ALGS[args.alg])
-    S.lib().shmemx_set_transport(0)
+    reset_transport(S, L)
     return out
 
 
@@ -486,8 +510,8 @@ def adjacent_collectives(args, torch, dist, L, S, dt, es, n, src, dst, stream, s
     # broadcast: the root puts the payload on its links once (scattered over P-1 links
     # above 64 KiB); each non-root forwards its 1/(P-1) share to the P-2 others
     colls.append(("broadcast_root0", lambda: bcast_fn(team, dst, src, n, 0), n * es))
-    for tname, tid in (("rccl", 0), ("p2p", 1)):
-        if S.lib().shmemx_set_transport(tid) < 0:
+    for tid, tname in enumerate(T_NAMES):
+        if not use_transport(S, L, tname):
             continue
         for cname, call, wire in colls:
             for _ in range(2):
@@ -537,7 +561,7 @@ def adjacent_collectives(args, torch, dist, L, S, dt, es, n, src, dst, stream, s
                 "wire_bytes_per_pe": int(wire),
                 "wire_GBs_per_pe": round(wire / ts / 1e9, 1),
                 "bitwise_mismatches_all_ranks": int(mmt.item())}
-    S.lib().shmemx_set_transport(0)
+    reset_transport(S, L)
     return out
 
 

@@ -18,12 +18,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OSHRUN = os.path.join(ROOT, "tools", "oshrun")
 
 
-def oshrun(np_, cmd, timeout=600):
+def oshrun(np_, cmd, timeout=600, extra_env=None):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     env.update({"SHMEMX_TRANSPORT": "p2p", "SHMEMX_DEVICE_HEAP_SIZE": "256M",
                 "SHMEMX_STAGE_BYTES": "64M", "SHMEMX_DEVICE": "0", "PYTHONPATH": ROOT})
+    env.update(extra_env or {})
     return subprocess.run([sys.executable, OSHRUN, "-np", str(np_), "--timeout", str(timeout - 30),
                            *cmd], capture_output=True, text=True, timeout=timeout, env=env)
 
@@ -55,12 +56,19 @@ def test_reduce_types_4_pes(examples):
     assert "reduce_types: OK (4 PEs)" in r.stdout
 
 
-@pytest.mark.parametrize("np_", [2, 3, 4, 8])
-def test_team_check(np_):
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900)
+@pytest.mark.parametrize("np_,signal", [(2, "stream"), (3, "stream"), (4, "stream"), (8, "stream"),
+                                         (3, "host"), (8, "host")])
+def test_team_check(np_, signal):
+    """Every schedule across np_ PE processes, with the p2p transport's counters moved by
+    stream-ordered device signals (the default) or by the host every round
+    (SHMEMX_P2P_SIGNAL=host)."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+               extra_env={"SHMEMX_P2P_SIGNAL": signal})
     # PEs print concurrently, so lines may interleave: count the reports, not lines
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
-    assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)\)", r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
+        r.stdout + r.stderr[-3000:]
+    assert {m for _, m in ok} == {signal}, ok
 
 
 @pytest.mark.parametrize("np_", [2, 3, 4, 8])
@@ -102,16 +110,20 @@ def test_bench_team_leg(np_):
     import json
     res = json.loads(lines[0])
     assert res["n_gpus"] == np_ and res["value"] > 0
-    assert res["config"]["transport"] == "p2p"
+    assert res["config"]["transport"] in ("p2p", "p2p_stream")
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0
-    for coll in res.get("adjacent_collectives", {}).get("p2p", {}).values():
-        assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]
-    assert res["host_resident"]["p2p"]["value_GiBs"] > 0, res["host_resident"]
-    for sched in ("rechalving", "recdbl_direct"):
-        assert res["schedules"]["p2p"][sched]["bitwise_mismatches_all_ranks"] == 0, res["schedules"]
-    curve = res["size_curve"]["p2p"]
-    assert [r["nreduce"] for r in curve] == [1 << 20, (1 << 20) + 3, 4 << 20]
-    assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
+    # both p2p signalling modes measured and checked in every leg
+    assert list(res["transports"]) == ["p2p", "p2p_stream"], res["transports"]
+    for t in ("p2p", "p2p_stream"):
+        assert res["transports"][t]["bitwise_mismatches_all_ranks"] == 0, res["transports"]
+        for coll in res["adjacent_collectives"][t].values():
+            assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]
+        assert res["host_resident"][t]["value_GiBs"] > 0, res["host_resident"]
+        for sched in ("rechalving", "recdbl_direct"):
+            assert res["schedules"][t][sched]["bitwise_mismatches_all_ranks"] == 0, res["schedules"]
+        curve = res["size_curve"][t]
+        assert [r["nreduce"] for r in curve] == [1 << 20, (1 << 20) + 3, 4 << 20]
+        assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
     # SOS's ring on np_ host processes beside the line, equal to the GPU ring byte for byte
     cpu = res["cpu_ring_baseline"]
     assert cpu["cores"] == np_ and cpu["value"] > 0 and cpu["kind"] == "port", cpu
@@ -206,6 +218,7 @@ def test_bench_team_leg_default_transport():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     import json
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
-    assert res["config"]["transport"] == "p2p" and list(res["transports"]) == ["p2p"]
+    assert res["config"]["transport"] in ("p2p", "p2p_stream")
+    assert list(res["transports"]) == ["p2p", "p2p_stream"]
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0
     assert "every PE runs on the p2p transport" in r.stderr

@@ -177,11 +177,12 @@ def main():
     S.shmem_free(psync)
     if even.value:
         S.lib().shmem_team_destroy(even)
+    sig = {1: "stream", 0: "host"}.get(L.lib().sosx_p2p_signal_mode(), "none")
     S.shmem_finalize()
     if bad:
         print(f"PE {me}/{P}: {len(bad)} of {checks} checks FAILED: {bad[:6]}", flush=True)
         return 1
-    print(f"PE {me}/{P}: {checks} checks OK", flush=True)
+    print(f"PE {me}/{P}: {checks} checks OK (p2p signal {sig})", flush=True)
     return 0
 
 
