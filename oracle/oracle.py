@@ -154,7 +154,8 @@ class PeRing:
         fd = os.open(path, os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0), 0o600)
         try:
             if create:
-                os.ftruncate(fd, size)
+                # reserve the pages now: a tmpfs that runs out later raises SIGBUS on touch
+                os.posix_fallocate(fd, 0, size)
             self.mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
         finally:
             os.close(fd)

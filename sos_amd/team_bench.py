@@ -286,15 +286,33 @@ def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed
     os.sched_setaffinity(0, {core})
     path = f"/dev/shm/sosx_cpu_ring_{os.environ.get('MASTER_PORT', '0')}_{world}"
     ring = None
+    why = ""
+
+    def agreed(ok):  # every rank learns whether all ranks succeeded
+        v = torch.tensor([0 if ok else 1], dtype=torch.int64)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        return v.item() == 0
+
     try:
+        ok = True
         if rank == 0:
-            if os.path.exists(path):
-                os.unlink(path)
-            ring = O.PeRing(path, world, 0, m, dt, create=True)
-        dist.barrier()
+            try:
+                if os.path.exists(path):
+                    os.unlink(path)
+                ring = O.PeRing(path, world, 0, m, dt, create=True)  # space reserved up front
+            except OSError as e:
+                ok, why = False, f"cannot create the {world}-PE segment: {e}"
+                if os.path.exists(path):
+                    os.unlink(path)
+        if not agreed(ok):
+            return {"skipped": why or "segment creation failed on rank 0"}
         if rank != 0:
-            ring = O.PeRing(path, world, rank, m, dt, create=False)
-        dist.barrier()
+            try:
+                ring = O.PeRing(path, world, rank, m, dt, create=False)
+            except OSError as e:
+                ok, why = False, str(e)
+        if not agreed(ok):
+            return {"skipped": why or "segment attach failed on a rank"}
         if rank == 0:
             os.unlink(path)  # every PE has it mapped
         host_src = O.fill(dt, dist_kind, seed, rank, m)
