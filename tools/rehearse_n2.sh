@@ -1,9 +1,16 @@
 #!/bin/bash
-cd "${GRAFT_REPO_ROOT}" || exit 1
+# Full-size rehearsal of the driver's N > 1 bench on ONE GPU (all ranks share it; RCCL
+# refuses that, so the job runs on the p2p transport in both signalling modes).
+# Usage: tools/rehearse_n2.sh [N ...]   (default: 2)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
-start=$(date +%s)
-timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 20 --warmup 5 > gpurun_out/n2.out 2> gpurun_out/n2.err
-rc=$?
-echo "rc=$rc wall=$(( $(date +%s) - start ))s"
-tail -3 gpurun_out/n2.err
-exit $rc
+for n in "${@:-2}"; do
+    start=$(date +%s)
+    timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
+        --master-addr 127.0.0.1 --master-port $((29555 + n)) bench.py --gpus "$n" --steps 20 \
+        --warmup 5 > "gpurun_out/n$n.out" 2> "gpurun_out/n$n.err"
+    rc=$?
+    echo "N=$n rc=$rc wall=$(( $(date +%s) - start ))s"
+    tail -3 "gpurun_out/n$n.err"
+    [ $rc -eq 0 ] || exit $rc
+done
