@@ -71,12 +71,17 @@ def test_team_check(np_, signal):
     assert {m for _, m in ok} == {signal}, ok
 
 
-@pytest.mark.parametrize("np_", [2, 3, 4, 8])
-def test_coll_check(np_):
-    """Scans and broadcasts through the public API (tools/coll_check.py)."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "coll_check.py")], timeout=900)
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
-    assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
+@pytest.mark.parametrize("np_,signal", [(2, "host"), (3, "host"), (4, "host"), (8, "host"),
+                                         (3, "stream"), (8, "stream")])
+def test_coll_check(np_, signal):
+    """Scans and broadcasts through the public API (tools/coll_check.py), p2p counters
+    moved by the host or by stream-ordered device signals."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "coll_check.py")], timeout=900,
+               extra_env={"SHMEMX_P2P_SIGNAL": signal})
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)\)", r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
+        r.stdout + r.stderr[-3000:]
+    assert {m for _, m in ok} == {signal}, ok
 
 
 @pytest.mark.parametrize("np_", [1, 2, 3, 4, 6])
@@ -179,23 +184,18 @@ def test_ipc_heap_sizes_with_bit31(heap):
     assert r.stdout.count("PE done") == 2, r.stdout
 
 
-@pytest.mark.parametrize("np_", [2, 3, 8])
-def test_team_check_host_stripes(np_):
+@pytest.mark.parametrize("np_,signal", [(2, "host"), (3, "host"), (8, "host"), (3, "stream")])
+def test_team_check_host_stripes(np_, signal):
     """Host-resident ring reductions pipelined in stripes (striped_host_ring): with 256-B
     chunk slices the host-buffer calls of tools/team_check.py run as many stripes plus
     the n mod P remainder stripe (p2p stripes only when SHMEMX_HOST_STRIPE_BYTES is set),
     bit for bit against the schedule-order fold."""
-    env_keep = os.environ.get("SHMEMX_HOST_STRIPE_BYTES")
-    os.environ["SHMEMX_HOST_STRIPE_BYTES"] = "256"
-    try:
-        r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900)
-    finally:
-        if env_keep is None:
-            os.environ.pop("SHMEMX_HOST_STRIPE_BYTES")
-        else:
-            os.environ["SHMEMX_HOST_STRIPE_BYTES"] = env_keep
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
-    assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+               extra_env={"SHMEMX_HOST_STRIPE_BYTES": "256", "SHMEMX_P2P_SIGNAL": signal})
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)\)", r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
+        r.stdout + r.stderr[-3000:]
+    assert {m for _, m in ok} == {signal}, ok
 
 
 def test_bench_team_leg_default_transport():
