@@ -171,6 +171,11 @@ int sosx_p2p_signal_mode(void);
  * its call sequence).  Returns the previous mode, or -1 when unavailable. */
 int sosx_set_p2p_signal_mode(int mode);
 
+/* RCCL executor: equal-chunk allgather rounds of world-team plans as one ncclAllGather
+ * (1) or as grouped send/receive pairs (0, default; SHMEMX_RCCL_ALLGATHER sets the
+ * start value).  Collective switch; returns the previous setting. */
+int sosx_set_rccl_allgather(int on);
+
 /* Kernel variant selection for the hot fp32/generic combine (bench/tuning only):
  * returns the previous variant.  0 = default. */
 int sosx_set_combine_variant(int variant);

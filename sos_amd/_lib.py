@@ -83,6 +83,7 @@ _SIGS = {
     "sosx_build_info": (_c.c_char_p, []),
     "sosx_p2p_signal_mode": (_c.c_int, []),
     "sosx_set_p2p_signal_mode": (_c.c_int, [_c.c_int]),
+    "sosx_set_rccl_allgather": (_c.c_int, [_c.c_int]),
 }
 
 

@@ -135,11 +135,54 @@ int run_locals(const sosplan::Round &r, const Bufs &b, int op, int dt, hipStream
     return SOSX_OK;
 }
 
+// Is round r, for this PE of the WORLD team, a pure allgather of equal chunks inside
+// DST: one send of this PE's chunk (bytes B at off0 + me*B) to every other PE and one
+// receive of PE q's chunk at off0 + q*B from every PE q, no local ops?  (The ring and
+// recdbl_direct plans' second round when P divides nreduce.)  Then RCCL's own
+// allgather moves exactly the bytes the send/receive pairs would.
+bool allgather_round(const sosplan::Round &r, const Team &t, uint64_t *off0, uint64_t *B)
+{
+    const State &s = st();
+    const int P = t.size, me = t.my_idx;
+    if (P < 2 || t.start != 0 || t.stride != 1 || P != s.n_pes || !r.ops.empty() ||
+        r.xfers.size() != 2 * (size_t)(P - 1))
+        return false;
+    uint64_t bytes = 0, base = 0;
+    bool have = false;
+    std::vector<char> sent((size_t)P, 0), got((size_t)P, 0);
+    for (const auto &x : r.xfers) {
+        if (x.buf != sosplan::DST || x.peer == me || x.peer < 0 || x.peer >= P) return false;
+        const int owner = x.send ? me : x.peer;
+        if (!have) {
+            bytes = x.bytes;
+            if (!bytes || x.off < (uint64_t)owner * bytes) return false;
+            base = x.off - (uint64_t)owner * bytes;
+            have = true;
+        }
+        if (x.bytes != bytes || x.off != base + (uint64_t)owner * bytes) return false;
+        char &seen = (x.send ? sent : got)[(size_t)x.peer];
+        if (seen) return false;
+        seen = 1;
+    }
+    *off0 = base;
+    *B = bytes;
+    return true;
+}
+
 // RCCL executor: one ncclGroup per round, folds after it, all on `stream`.
 int exec_rccl(const Plan &p, const Team &t, const Bufs &b, int op, int dt, hipStream_t stream)
 {
     State &s = st();
     for (const auto &r : p.rounds) {
+        uint64_t off0 = 0, B = 0;
+        if (s.rccl_allgather && allgather_round(r, t, &off0, &B)) {
+            if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, false), stream);
+            char *base = b.wat(sosplan::DST, off0);
+            if (ncclAllGather(base + (size_t)t.my_idx * B, base, B, ncclUint8, s.comm, stream) != ncclSuccess)
+                return SOSX_ERR_RCCL;
+            if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, true), stream);
+            continue;
+        }
         if (!r.xfers.empty()) {
             if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, false), stream);
             if (ncclGroupStart() != ncclSuccess) return SOSX_ERR_RCCL;

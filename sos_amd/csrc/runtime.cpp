@@ -159,6 +159,8 @@ static void read_env(State &s)
     s.host_stripe_bytes = atol_scaled(getenv("SHMEMX_HOST_STRIPE_BYTES"), 256u << 10);
     s.host_stripe_explicit = getenv("SHMEMX_HOST_STRIPE_BYTES") != nullptr;
     s.sym_stage_bytes = atol_scaled(getenv("SHMEMX_STAGE_BYTES"), 512ull << 20);
+    const char *ag = getenv("SHMEMX_RCCL_ALLGATHER");
+    s.rccl_allgather = ag && atoi(ag) != 0;
     s.sym_stage_bytes = (s.sym_stage_bytes + 4095) & ~(size_t)4095;
     if (s.sym_stage_bytes >= s.dev_heap_bytes) s.dev_heap_bytes = s.sym_stage_bytes + (256u << 20);
 }
@@ -810,6 +812,17 @@ int shmemx_set_transport(int transport)
     else if (transport == TRANSPORT_P2P && s.p2p_ready && (s.shm.base || s.n_pes == 1))
         s.transport = TRANSPORT_P2P;
     else return -1;
+    return prev;
+}
+
+// RCCL executor: run equal-chunk allgather rounds of world-team plans as ncclAllGather
+// (1) or as grouped send/receive pairs (0, the default).  Same bytes either way; every
+// PE must switch at the same point of its call sequence.  Returns the previous setting.
+int sosx_set_rccl_allgather(int on)
+{
+    State &s = st();
+    const int prev = s.rccl_allgather ? 1 : 0;
+    s.rccl_allgather = on != 0;
     return prev;
 }
 

@@ -98,6 +98,8 @@ struct State {
     sosboot::Hub hub;                 // TCP star to PE 0 (shmem_init path)
     sosboot::ShmBarrier shm;          // node-local barrier + transport counters
     int transport = TRANSPORT_RCCL;   // the transport calls use now
+    bool rccl_allgather = false;      // SHMEMX_RCCL_ALLGATHER: equal-chunk allgather rounds
+                                      // of a world-team plan as one ncclAllGather
     bool want_rccl = true;            // create the RCCL communicator
     bool want_p2p = false;            // IPC-map the device heap on every PE
     bool p2p_ready = false;           // heap mapped (or single PE)

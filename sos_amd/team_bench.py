@@ -10,7 +10,8 @@ Both inter-PE transports are measured (SHMEMX_TRANSPORT=both):
   rccl       : ncclSend/ncclRecv over xGMI + the HIP fold kernels (the library default)
   p2p        : the fold kernel reads the peers' chunks straight out of their IPC-mapped
                HBM; the host moves the transfer counters every round
-  p2p_stream : the same with stream-ordered device signals (one host sync per call)
+  rccl_ag    : the same, the allgather round as one ncclAllGather when chunks are equal
+  p2p_stream : p2p with stream-ordered device signals (one host sync per call)
 `value` is the fastest one whose bitwise check is clean.
 Self-check: after timing, every rank regenerates all P inputs on its own GPU and
 re-evaluates the schedule's element order with the fold kernel (ring: chunk c folded
@@ -31,23 +32,28 @@ XGMI_LINK_GBS = 153.0   # per link, per direction, nominal
 XGMI_LINKS = 7
 
 
-# Measured transports: (name, shmemx_set_transport id, p2p signalling mode).  p2p runs
-# twice: counters moved by the host every round (the default) and by stream-ordered
-# device signals (sosx_set_p2p_signal_mode(1)); every leg reports each one.
-TRANSPORTS = (("rccl", 0, None), ("p2p", 1, 0), ("p2p_stream", 1, 1))
+# Measured transports: (name, shmemx_set_transport id, p2p signalling mode, RCCL native
+# allgather).  rccl runs twice: every round as grouped ncclSend/ncclRecv (the default) and
+# with the equal-chunk allgather round as one ncclAllGather (sosx_set_rccl_allgather);
+# p2p runs twice: counters moved by the host every round (the default) and by
+# stream-ordered device signals (sosx_set_p2p_signal_mode(1)).  Every leg reports each.
+TRANSPORTS = (("rccl", 0, None, 0), ("rccl_ag", 0, None, 1), ("p2p", 1, 0, 0),
+              ("p2p_stream", 1, 1, 0))
 T_NAMES = tuple(t[0] for t in TRANSPORTS)
 
 
 def use_transport(S, L, tname):
     """Switch every PE (collectively) to `tname`; False when it is unavailable."""
-    _, tid, sig = next(t for t in TRANSPORTS if t[0] == tname)
+    _, tid, sig, ag = next(t for t in TRANSPORTS if t[0] == tname)
     if S.lib().shmemx_set_transport(tid) < 0:
         return False
+    L.lib().sosx_set_rccl_allgather(ag)
     return sig is None or L.lib().sosx_set_p2p_signal_mode(sig) >= 0
 
 
 def reset_transport(S, L):
     S.lib().shmemx_set_transport(0)
+    L.lib().sosx_set_rccl_allgather(0)
     L.lib().sosx_set_p2p_signal_mode(0)
 
 
@@ -206,7 +212,7 @@ def main(args, torch):
         "data": "synthetic (splitmix64 counter hash per PE, SURVEY.md 8(d)), resident in HBM",
         "config": {"workload": f"shmem_{args.dtype}_{args.op}_reduce(SHMEM_TEAM_WORLD) nreduce={n} "
                                f"per PE, {world} PEs (1 per MI355X), "
-                               + ("RCCL over xGMI + HIP fold" if primary == "rccl" else
+                               + ("RCCL over xGMI + HIP fold" if primary.startswith("rccl") else
                                   "p2p reads of IPC-mapped peer HBM + HIP fold"
                                   + (", stream-ordered signals" if primary == "p2p_stream" else "")),
                    "nreduce": n, "algorithm": name, "transport": primary,
@@ -224,7 +230,8 @@ def main(args, torch):
     res["transports"] = {k: team_roof(results[k]) for k in measured}
     res["transport_choice"] = ("value = the faster of the measured transports with a clean "
                                "bitwise check; the library default is rccl "
-                               "(SHMEMX_TRANSPORT selects; p2p_stream = p2p with "
+                               "(SHMEMX_TRANSPORT selects; rccl_ag = rccl with "
+                               "SHMEMX_RCCL_ALLGATHER=1, p2p_stream = p2p with "
                                "SHMEMX_P2P_SIGNAL=stream)")
     if curve:
         res["size_curve"] = curve

@@ -1,8 +1,8 @@
 // TEST INFRASTRUCTURE ONLY -- never linked into sos_amd/libsos_amd.so.
 //
-// A stand-in for the eight RCCL entry points libsos_amd.so calls (ncclGetUniqueId,
+// A stand-in for the nine RCCL entry points libsos_amd.so calls (ncclGetUniqueId,
 // ncclCommInitRank, ncclCommDestroy, ncclGetErrorString, ncclGroupStart/End, ncclSend,
-// ncclRecv), linked with hidden visibility into a test copy of the library,
+// ncclRecv, ncclAllGather), linked with hidden visibility into a test copy of the library,
 // tests/fakerccl/libsos_amd_fakerccl.so.  Real RCCL refuses two ranks on one GPU
 // ("Duplicate GPU detected"), and the GPU box has one, so without this the RCCL executor
 // (collectives.cpp exec_rccl, the RCCL device barrier and team words in runtime.cpp) only
@@ -17,6 +17,8 @@
 //     /dev/shm/fakerccl_<id>_<src>_<dst>_<seq> (written under a temporary name, then
 //     renamed), then waits for each receive's file, copies it into the receive buffer
 //     and unlinks it.  It returns with all transfers complete.
+//   * ncclAllGather is a group of one send of the contribution to every peer and one
+//     receive from every peer into its slot, plus the local copy when not in place;
 //   * messages of one ordered pair match in issue order through per-pair sequence numbers,
 //     RCCL's FIFO rule; a size mismatch or a wait longer than FAKERCCL_TIMEOUT seconds
 //     (default 120) returns an error, which libsos_amd.so turns into an abort.
@@ -54,7 +56,7 @@ struct Op {
 
 int g_depth = 0;
 std::vector<Op> g_ops;
-unsigned long long g_msgs = 0, g_bytes = 0;
+unsigned long long g_msgs = 0, g_bytes = 0, g_allgathers = 0;
 int g_rank = -1;
 
 // FAKERCCL_STATS=1: each process reports how much went through the stand-in, so a test can
@@ -63,8 +65,8 @@ __attribute__((destructor)) void report()
 {
     const char *e = getenv("FAKERCCL_STATS");
     if (e && *e == '1' && g_rank >= 0)
-        fprintf(stderr, "fakerccl stats: rank %d sent %llu messages, %llu bytes\n", g_rank, g_msgs,
-                g_bytes);
+        fprintf(stderr, "fakerccl stats: rank %d sent %llu messages, %llu bytes, %llu allgathers\n",
+                g_rank, g_msgs, g_bytes, g_allgathers);
 }
 
 double now_s()
@@ -269,4 +271,26 @@ ncclResult_t ncclRecv(void *buf, size_t count, ncclDataType_t t, int peer, ncclC
                       hipStream_t stream)
 {
     return enqueue(false, buf, count, t, peer, comm, stream);
+}
+
+ncclResult_t ncclAllGather(const void *sendbuff, void *recvbuff, size_t sendcount,
+                           ncclDataType_t t, ncclComm_t comm, hipStream_t stream)
+{
+    const size_t ts = type_size(t);
+    if (!comm || !ts || g_depth) return ncclInvalidArgument;
+    const size_t bytes = sendcount * ts;
+    char *mine = (char *)recvbuff + (size_t)comm->rank * bytes;
+    ++g_allgathers;
+    ncclGroupStart();
+    for (int q = 0; q < comm->nranks; ++q) {
+        if (q == comm->rank) continue;
+        enqueue(true, sendbuff, sendcount, t, q, comm, stream);
+        enqueue(false, (char *)recvbuff + (size_t)q * bytes, sendcount, t, q, comm, stream);
+    }
+    const ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) return r;
+    if (mine != sendbuff && bytes &&
+        hipMemcpyAsync(mine, sendbuff, bytes, hipMemcpyDefault, stream) != hipSuccess)
+        return ncclUnhandledCudaError;
+    return ncclSuccess;
 }

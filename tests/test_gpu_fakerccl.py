@@ -2,7 +2,7 @@
 
 Real RCCL refuses two ranks on one GPU, so these runs load a test build of the library,
 tests/fakerccl/libsos_amd_fakerccl.so: the same objects as sos_amd/libsos_amd.so, with the
-eight RCCL entry points it calls bound to tests/fakerccl/fake_rccl.cpp, which moves each
+nine RCCL entry points it calls bound to tests/fakerccl/fake_rccl.cpp, which moves each
 ncclSend/ncclRecv through a /dev/shm file with RCCL's per-pair FIFO matching.  Everything
 above those calls is the product code the 8-GPU node runs with SHMEMX_TRANSPORT=rccl: the
 plans, exec_rccl's byte offsets and groups, the folds between rounds, the striped
@@ -72,6 +72,19 @@ def test_team_check_rccl_executor(np_):
     _ok(r, np_)
 
 
+@pytest.mark.parametrize("np_", [2, 4])
+def test_team_check_rccl_native_allgather(np_):
+    """SHMEMX_RCCL_ALLGATHER=1: equal-chunk allgather rounds of world-team plans go through
+    ncclAllGather (counted by the stand-in); every check stays bit-exact."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+               SHMEMX_RCCL_ALLGATHER="1")
+    _ok(r, np_)
+    ag = {int(rk): int(a) for rk, a in
+          re.findall(r"fakerccl stats: rank (\d+) sent \d+ messages, \d+ bytes, (\d+) allgathers",
+                     r.stderr)}
+    assert sorted(ag) == list(range(np_)) and min(ag.values()) > 0, r.stderr[-2000:]
+
+
 @pytest.mark.parametrize("np_", [3])
 def test_coll_check_rccl_executor(np_):
     """Scans and broadcasts over the RCCL executor."""
@@ -105,15 +118,18 @@ def test_bench_team_leg_rccl():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     _used_fake(r, 2)
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
-    assert res["config"]["transport"] == "rccl", res["config"]
+    assert res["config"]["transport"] in ("rccl", "rccl_ag"), res["config"]
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0, res["check"]
-    for coll in res.get("adjacent_collectives", {}).get("rccl", {}).values():
-        assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]
-    assert res["host_resident"]["rccl"]["value_GiBs"] > 0, res["host_resident"]
-    for sched in ("rechalving", "recdbl_direct"):
-        assert res["schedules"]["rccl"][sched]["bitwise_mismatches_all_ranks"] == 0, res["schedules"]
-    curve = res["size_curve"]["rccl"]
-    assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
+    assert list(res["transports"]) == ["rccl", "rccl_ag"], res["transports"]
+    for t in ("rccl", "rccl_ag"):
+        assert res["transports"][t]["bitwise_mismatches_all_ranks"] == 0, res["transports"]
+        for coll in res["adjacent_collectives"][t].values():
+            assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]
+        assert res["host_resident"][t]["value_GiBs"] > 0, res["host_resident"]
+        for sched in ("rechalving", "recdbl_direct"):
+            assert res["schedules"][t][sched]["bitwise_mismatches_all_ranks"] == 0, res["schedules"]
+        curve = res["size_curve"][t]
+        assert curve[-1]["bitwise_mismatches_all_ranks"] == 0   # 4Mi: equal chunks
 
 
 @pytest.mark.parametrize("script", ["team_check.py", "team_mgmt_check.py"])

@@ -13,6 +13,10 @@ class _Lib:
         self.calls.append(("transport", tid))
         return 0 if tid in self.transports_ok else -1
 
+    def sosx_set_rccl_allgather(self, on):
+        self.calls.append(("allgather", on))
+        return 0
+
     def sosx_set_p2p_signal_mode(self, mode):
         self.calls.append(("signal", mode))
         return -1 if (mode == 1 and not self.stream_ok) else 0
@@ -29,15 +33,18 @@ class _Wrap:
 def test_use_transport_selects_transport_and_signal_mode():
     lib = _Lib({0, 1}, stream_ok=True)
     S = L = _Wrap(lib)
-    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [True, True, True]
-    assert lib.calls == [("transport", 0), ("transport", 1), ("signal", 0), ("transport", 1),
-                         ("signal", 1)]
+    assert TB.T_NAMES == ("rccl", "rccl_ag", "p2p", "p2p_stream")
+    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [True, True, True, True]
+    assert lib.calls == [("transport", 0), ("allgather", 0),
+                         ("transport", 0), ("allgather", 1),
+                         ("transport", 1), ("allgather", 0), ("signal", 0),
+                         ("transport", 1), ("allgather", 0), ("signal", 1)]
     lib.calls.clear()
     TB.reset_transport(S, L)
-    assert lib.calls == [("transport", 0), ("signal", 0)]
+    assert lib.calls == [("transport", 0), ("allgather", 0), ("signal", 0)]
 
 
 def test_unavailable_transports_report_false():
     lib = _Lib({1}, stream_ok=False)   # RCCL down, stream signalling unavailable
     S = L = _Wrap(lib)
-    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [False, True, False]
+    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [False, False, True, False]

@@ -23,7 +23,7 @@ from sos_amd import shmem as S  # noqa: E402
 CASES = [("float", "sum"), ("double", "prod"), ("int64", "xor"), ("int", "max"), ("complexd", "prod"),
          ("short", "sum"), ("uint8", "min"), ("ulong", "or")]
 ALGS = ["auto", "ring", "recdbl", "rechalving", "recdbl_direct", "recdbl_gather"]
-SIZES = [1, 37, 5003, (1 << 20) + 3]
+SIZES = [1, 37, 5003, 65536, (1 << 20) + 3]  # 65536: equal ring chunks for P | 65536
 
 
 def expected(dt, opid, dist, seed, members, my_idx, n, es, alg_resolved, pe_of):
