@@ -25,13 +25,14 @@
 // chunks -- the RCCL version's scratch round trip disappears.
 //
 // Two signalling modes, agreed by every PE when the heap is mapped:
-//   stream (default): the counters move in stream order, written and awaited by a
-//     one-workgroup kernel (sosx_p2p_signal) on host-registered node shared memory.  A
-//     call enqueues all of its rounds at once -- signal, folds/gathers, signal, ... --
-//     and the host synchronises once, at the end.  Each PE's buffer offsets for the
+//   stream (the default): between rounds the counters move in stream
+//     order, written and awaited by a one-workgroup kernel (sosx_p2p_signal) on
+//     host-registered node shared memory, so the rounds are enqueued back to back and
+//     the host synchronises once.  The call's entry and exit boundaries stay on the
+//     host (there is nothing queued for a signal kernel to overlap there).  Each PE's buffer offsets for the
 //     call travel ahead of the data through a small descriptor ring per ordered pair
 //     (host handshake only, never waiting on a GPU).
-//   host (SHMEMX_P2P_SIGNAL=host, or HIP cannot register the segment): the host
+//   host (SHMEMX_P2P_SIGNAL=host, or when HIP cannot register the segment): the host
 //     synchronises the stream and moves the counters itself every round, as steps 1-4.
 #include <time.h>
 #include <hip/hip_runtime.h>
@@ -143,6 +144,26 @@ void spin_until(std::atomic<uint64_t> &a, uint64_t want, const char *what)
     unsigned spins = 0;
     double t0 = 0;
     while (a.load(std::memory_order_acquire) < want) {
+        if (++spins < 4096) {
+            __builtin_ia32_pause();
+            continue;
+        }
+        sched_yield();
+        if ((spins & 1023) == 0) {
+            const double t = now_s();
+            if (t0 == 0) t0 = t;
+            else if (t - t0 > wait_limit_s())
+                raise_error("p2p transport: timed out after %.0f s waiting for %s", t - t0, what);
+        }
+    }
+}
+
+// The same bound for a counter the GPUs also write (stream mode).
+void spin_until_u64(const uint64_t *a, uint64_t want, const char *what)
+{
+    unsigned spins = 0;
+    double t0 = 0;
+    while (__atomic_load_n(a, __ATOMIC_ACQUIRE) < want) {
         if (++spins < 4096) {
             __builtin_ia32_pause();
             continue;
@@ -349,7 +370,16 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
         return sosx_p2p_signal((int)wa.size(), wa.data(), wv.data(), (int)qa.size(), qa.data(),
                                qv.data(), dev(&sh->sig_err[my_world]), g_sig.limit_ticks, stream);
     };
+    // the same step done by the host (the call's first and last boundaries, where the
+    // host has nothing to overlap: stores, then bounded waits)
+    auto host_flush = [&]() {
+        for (auto &kv : pw_store) __atomic_store_n(kv.first, kv.second, __ATOMIC_RELEASE);
+        for (auto &kv : pw_wait) spin_until_u64(kv.first, kv.second, "a peer (call boundary)");
+        pw_store.clear();
+        pw_wait.clear();
+    };
     std::vector<int> recv_idx((size_t)t.size, 0);  // k-th receive from each team peer
+    bool first_xfer_round = true;
     for (const auto &r : plan.rounds) {
         if (r.xfers.empty()) {
             int rc = flush();
@@ -372,8 +402,20 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
                 pw_wait[&sh->dposted[pw][my_world]] = ++g_sig.seen[pw];
             }
         }
-        int rc = flush();
-        if (rc) return rc;
+        int rc;
+        if (first_xfer_round) {
+            // the call's entry boundary runs on the host, as in host mode: nothing is
+            // queued ahead of it that a signal kernel could overlap (stream sync only
+            // when this round sends, so that the posted bytes are final)
+            first_xfer_round = false;
+            bool sends = false;
+            for (const auto &x : r.xfers) sends |= x.send != 0;
+            if (sends && hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
+            host_flush();
+        } else {
+            rc = flush();
+            if (rc) return rc;
+        }
         struct Seg { const char *src; char *dst; uint64_t bytes; bool used; };
         std::vector<Seg> segs;
         for (const auto &x : r.xfers) {
@@ -438,14 +480,14 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
             if (rc) return rc;
         }
     }
-    int rc = flush();
-    if (rc) return rc;
+    // the exit boundary (the last round's consumed marks) on the host, after the sync
     phase(PH_ENQUEUE);
     const hipError_t e = hipStreamSynchronize(stream);
-    phase(PH_SYNC_END);
     if (__atomic_load_n(&sh->sig_err[my_world], __ATOMIC_ACQUIRE))
         raise_error("p2p transport: timed out after %.0f s waiting for a peer (device wait)",
                     wait_limit_s());
+    if (e == hipSuccess) host_flush();
+    phase(PH_SYNC_END);
     if (tr && ++g_trace.calls % g_trace.every == 0) {
         const double k = 1e6 / (double)g_trace.every;
         fprintf(stderr, "[%04d] p2p trace, stream mode (calls %ld-%ld, us/call): descriptors %.1f "
@@ -461,9 +503,10 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
 
 // Signalling setup (runtime.cpp ensure_device_heap, collective): register the shared
 // segment with HIP on every PE and agree through the bootstrap whether stream mode is
-// possible everywhere.  The mode in use starts as SHMEMX_P2P_SIGNAL (host by default:
-// on one GPU shared by 2 or 8 PE processes the host mode measured faster, profiles/
-// r2_p2p_signal_latency.txt) and can be switched collectively (sosx_set_p2p_signal_mode).
+// possible everywhere.  The mode in use starts as SHMEMX_P2P_SIGNAL (stream by default
+// when every PE can: equal or faster than host mode in every one-GPU measurement,
+// profiles/r2_p2p_signal_latency.txt) and can be switched collectively
+// (sosx_set_p2p_signal_mode).
 void p2p_signal_setup()
 {
     State &s = st();
@@ -504,7 +547,7 @@ void p2p_signal_setup()
     g_sig.dbase = (char *)dptr;
     g_sig.limit_ticks = (long long)(wait_limit_s() * 1e3 * (double)rate_khz);
     const char *e = getenv("SHMEMX_P2P_SIGNAL");  // the same on every PE (job environment)
-    g_sig.on = g_sig.capable && e && strcmp(e, "stream") == 0;
+    g_sig.on = g_sig.capable && !(e && strcmp(e, "host") == 0);
     debug_msg("p2p transport signalling: %s (stream mode %s)", g_sig.on ? "stream" : "host",
               g_sig.capable ? "available" : "unavailable");
 }

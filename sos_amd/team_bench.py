@@ -9,9 +9,9 @@ is libsos_amd.so behind the public C API: shmem_init() bootstraps over TCP
 Both inter-PE transports are measured (SHMEMX_TRANSPORT=both):
   rccl       : ncclSend/ncclRecv over xGMI + the HIP fold kernels (the library default)
   p2p        : the fold kernel reads the peers' chunks straight out of their IPC-mapped
-               HBM; the host moves the transfer counters every round
+               HBM; stream-ordered signals between rounds (one host sync per call)
   rccl_ag    : the same, the allgather round as one ncclAllGather when chunks are equal
-  p2p_stream : p2p with stream-ordered device signals (one host sync per call)
+  p2p_host   : p2p with the host moving the transfer counters every round
 `value` is the fastest one whose bitwise check is clean.
 Self-check: after timing, every rank regenerates all P inputs on its own GPU and
 re-evaluates the schedule's element order with the fold kernel (ring: chunk c folded
@@ -35,10 +35,11 @@ XGMI_LINKS = 7
 # Measured transports: (name, shmemx_set_transport id, p2p signalling mode, RCCL native
 # allgather).  rccl runs twice: every round as grouped ncclSend/ncclRecv (the default) and
 # with the equal-chunk allgather round as one ncclAllGather (sosx_set_rccl_allgather);
-# p2p runs twice: counters moved by the host every round (the default) and by
-# stream-ordered device signals (sosx_set_p2p_signal_mode(1)).  Every leg reports each.
-TRANSPORTS = (("rccl", 0, None, 0), ("rccl_ag", 0, None, 1), ("p2p", 1, 0, 0),
-              ("p2p_stream", 1, 1, 0))
+# p2p runs twice: counters moved between rounds by stream-ordered device signals (the
+# default) and by the host every round (sosx_set_p2p_signal_mode(0)).  Every leg
+# reports each.
+TRANSPORTS = (("rccl", 0, None, 0), ("rccl_ag", 0, None, 1), ("p2p", 1, 1, 0),
+              ("p2p_host", 1, 0, 0))
 T_NAMES = tuple(t[0] for t in TRANSPORTS)
 
 
@@ -54,7 +55,7 @@ def use_transport(S, L, tname):
 def reset_transport(S, L):
     S.lib().shmemx_set_transport(0)
     L.lib().sosx_set_rccl_allgather(0)
-    L.lib().sosx_set_p2p_signal_mode(0)
+    L.lib().sosx_set_p2p_signal_mode(1)
 
 
 def log(*a):
@@ -214,7 +215,7 @@ def main(args, torch):
                                f"per PE, {world} PEs (1 per MI355X), "
                                + ("RCCL over xGMI + HIP fold" if primary.startswith("rccl") else
                                   "p2p reads of IPC-mapped peer HBM + HIP fold"
-                                  + (", stream-ordered signals" if primary == "p2p_stream" else "")),
+                                  + (", host-signalled rounds" if primary == "p2p_host" else "")),
                    "nreduce": n, "algorithm": name, "transport": primary,
                    "parallelism": f"pe{world}"},
         "roofline": {"bound": "hbm", "kernel": "sos::k_fold (fused P-way combine)",
@@ -231,8 +232,8 @@ def main(args, torch):
     res["transport_choice"] = ("value = the faster of the measured transports with a clean "
                                "bitwise check; the library default is rccl "
                                "(SHMEMX_TRANSPORT selects; rccl_ag = rccl with "
-                               "SHMEMX_RCCL_ALLGATHER=1, p2p_stream = p2p with "
-                               "SHMEMX_P2P_SIGNAL=stream)")
+                               "SHMEMX_RCCL_ALLGATHER=1, p2p_host = p2p with "
+                               "SHMEMX_P2P_SIGNAL=host)")
     if curve:
         res["size_curve"] = curve
     if schedules:

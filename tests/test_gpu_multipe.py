@@ -115,11 +115,11 @@ def test_bench_team_leg(np_):
     import json
     res = json.loads(lines[0])
     assert res["n_gpus"] == np_ and res["value"] > 0
-    assert res["config"]["transport"] in ("p2p", "p2p_stream")
+    assert res["config"]["transport"] in ("p2p", "p2p_host")
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0
     # both p2p signalling modes measured and checked in every leg
-    assert list(res["transports"]) == ["p2p", "p2p_stream"], res["transports"]
-    for t in ("p2p", "p2p_stream"):
+    assert list(res["transports"]) == ["p2p", "p2p_host"], res["transports"]
+    for t in ("p2p", "p2p_host"):
         assert res["transports"][t]["bitwise_mismatches_all_ranks"] == 0, res["transports"]
         for coll in res["adjacent_collectives"][t].values():
             assert coll["bitwise_mismatches_all_ranks"] == 0, res["adjacent_collectives"]
@@ -218,7 +218,7 @@ def test_bench_team_leg_default_transport():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     import json
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
-    assert res["config"]["transport"] in ("p2p", "p2p_stream")
-    assert list(res["transports"]) == ["p2p", "p2p_stream"]
+    assert res["config"]["transport"] in ("p2p", "p2p_host")
+    assert list(res["transports"]) == ["p2p", "p2p_host"]
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0
     assert "every PE runs on the p2p transport" in r.stderr

@@ -33,18 +33,18 @@ class _Wrap:
 def test_use_transport_selects_transport_and_signal_mode():
     lib = _Lib({0, 1}, stream_ok=True)
     S = L = _Wrap(lib)
-    assert TB.T_NAMES == ("rccl", "rccl_ag", "p2p", "p2p_stream")
+    assert TB.T_NAMES == ("rccl", "rccl_ag", "p2p", "p2p_host")
     assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [True, True, True, True]
     assert lib.calls == [("transport", 0), ("allgather", 0),
                          ("transport", 0), ("allgather", 1),
-                         ("transport", 1), ("allgather", 0), ("signal", 0),
-                         ("transport", 1), ("allgather", 0), ("signal", 1)]
+                         ("transport", 1), ("allgather", 0), ("signal", 1),
+                         ("transport", 1), ("allgather", 0), ("signal", 0)]
     lib.calls.clear()
     TB.reset_transport(S, L)
-    assert lib.calls == [("transport", 0), ("allgather", 0), ("signal", 0)]
+    assert lib.calls == [("transport", 0), ("allgather", 0), ("signal", 1)]
 
 
 def test_unavailable_transports_report_false():
     lib = _Lib({1}, stream_ok=False)   # RCCL down, stream signalling unavailable
     S = L = _Wrap(lib)
-    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [False, False, True, False]
+    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [False, False, False, True]
