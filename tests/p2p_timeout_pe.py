@@ -1,0 +1,31 @@
+"""Run under tools/oshrun with 2 PEs (p2p transport): PE 1 reaches the reduction 60 s
+late; PE 0, with SHMEMX_P2P_TIMEOUT=3, must end the job with the p2p timeout error
+instead of hanging (tests/test_gpu_multipe.py::test_p2p_wait_is_bounded)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402,F401
+
+from sos_amd import shmem as S  # noqa: E402
+
+
+def main():
+    S.shmem_init()
+    me = S.shmem_my_pe()
+    n = 1 << 16
+    src = S.shmemx_malloc_device(n * 4)
+    dst = S.shmemx_malloc_device(n * 4)
+    S.shmem_barrier_all()
+    if me == 1:
+        time.sleep(60)
+    S.shmem_float_sum_reduce(S.team_world(), dst, src, n)
+    print(f"PE {me}: reduction returned", flush=True)
+    S.shmem_finalize()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

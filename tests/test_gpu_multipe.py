@@ -10,6 +10,7 @@ import os
 import re
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -82,6 +83,19 @@ def test_coll_check(np_, signal):
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
         r.stdout + r.stderr[-3000:]
     assert {m for _, m in ok} == {signal}, ok
+
+
+@pytest.mark.parametrize("signal", ["stream", "host"])
+def test_p2p_wait_is_bounded(signal):
+    """A PE that never arrives ends the job with the p2p timeout error (SHMEMX_P2P_TIMEOUT)
+    on the waiting PE, in both signalling modes, instead of a hang."""
+    t0 = time.monotonic()
+    r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "p2p_timeout_pe.py")], timeout=150,
+               extra_env={"SHMEMX_P2P_TIMEOUT": "3", "SHMEMX_P2P_SIGNAL": signal})
+    assert r.returncode != 0, r.stdout
+    assert "p2p transport: timed out" in r.stderr, r.stderr[-2000:]
+    assert "reduction returned" not in r.stdout
+    assert time.monotonic() - t0 < 55, "the job outlived the late PE's sleep"
 
 
 @pytest.mark.parametrize("np_", [1, 2, 3, 4, 6])
