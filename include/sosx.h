@@ -164,6 +164,13 @@ int sosx_p2p_signal(int nw, uint64_t *const *waddr, const uint64_t *wval, int nq
                     const uint64_t *const *qaddr, const uint64_t *qval, uint64_t *err,
                     long long limit_ticks, void *stream);
 
+/* sosx_gather preceded by such a signalling step (at most 16 stores and 16 waits); a
+ * small grid carries the step inside the copy launch. */
+int sosx_gather_signalled(int nseg, const void *const *srcs, void *const *dsts,
+                          const size_t *bytes, int nw, uint64_t *const *waddr,
+                          const uint64_t *wval, int nq, const uint64_t *const *qaddr,
+                          const uint64_t *qval, uint64_t *err, long long limit_ticks, void *stream);
+
 /* The p2p transport's signalling mode: 1 = stream-ordered device signals, 0 = host
  * synchronisation every round (SHMEMX_P2P_SIGNAL=host), -1 = no p2p transport. */
 int sosx_p2p_signal_mode(void);

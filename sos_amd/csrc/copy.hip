@@ -12,6 +12,51 @@ namespace sos {
 
 constexpr int kMaxSeg = 16;
 
+// ---------------------------------------------------------------------------------
+// Stream-ordered signalling of the peer-to-peer transport (p2p.cpp): one lane per
+// counter.  Lanes first store their new counter values (monotonic transfer counters in
+// node shared memory, registered with HIP so the GPU reaches them), then every lane
+// waits until its counter reaches its wanted value.  Because the launch sits in stream
+// order, the stores happen after the kernels that produced the sent bytes and the
+// waits hold back the kernels that read a peer's bytes.  Every wait is bounded by
+// `limit` wall-clock ticks: on expiry the lane sets *err and returns, so the grid
+// always drains (the host turns *err into an error after the stream synchronises).
+// ---------------------------------------------------------------------------------
+constexpr int kMaxSig = 64;
+
+// Lane i < nw stores its counter, then lane i < nq waits for its counter (bounded).
+template <int N> struct Sig {
+    uint64_t *waddr[N];
+    uint64_t wval[N];
+    const uint64_t *qaddr[N];
+    uint64_t qval[N];
+    uint64_t *err;
+    long long limit;
+    int nw, nq;
+};
+
+template <int N> __device__ __forceinline__ void sig_step(const Sig<N> &a, int i)
+{
+    if (i < a.nw) __hip_atomic_store(a.waddr[i], a.wval[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (i < a.nq) {
+        const long long t0 = wall_clock64();
+        while (__hip_atomic_load(a.qaddr[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.qval[i]) {
+            if (wall_clock64() - t0 > a.limit) {
+                __hip_atomic_store(a.err, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+
+using SigArgs = Sig<kMaxSig>;
+
+__global__ __launch_bounds__(kMaxSig) void k_p2p_signal(SigArgs a) { sig_step(a, threadIdx.x); }
+
+
 struct GatherArgs {
     const char *src[kMaxSeg];
     char *dst[kMaxSeg];
@@ -22,8 +67,19 @@ struct GatherArgs {
     int nseg;
 };
 
-__global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g)
+// A gather whose launch also carries the preceding p2p signalling step: every workgroup
+// stores the counters (idempotent) and waits for its own view of the awaited ones
+// before copying, so no workgroup depends on another being resident.  Only for grids
+// of at most 16 workgroups (<= 256 KiB): waiting workgroups hold their CUs, and with
+// several PEs on one GPU 256-workgroup gates starved the peers' kernels (a 4 MiB ring
+// call at P = 2 took 67 us instead of 30, profiles/r2_p2p_signal_latency.txt).
+constexpr int kMaxGate = 16;
+constexpr unsigned kGateMaxBlocks = 16;
+
+template <bool GATED>
+__global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g, Sig<kMaxGate> gate)
 {
+    if constexpr (GATED) sig_step(gate, threadIdx.x);
     const uint64_t total = g.vstart[g.nseg];
     const uint64_t stride = (uint64_t)gridDim.x * kThreads;
     int s = 0;
@@ -45,57 +101,40 @@ __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g)
     }
 }
 
-// ---------------------------------------------------------------------------------
-// Stream-ordered signalling of the peer-to-peer transport (p2p.cpp): one lane per
-// counter.  Lanes first store their new counter values (monotonic transfer counters in
-// node shared memory, registered with HIP so the GPU reaches them), then every lane
-// waits until its counter reaches its wanted value.  Because the launch sits in stream
-// order, the stores happen after the kernels that produced the sent bytes and the
-// waits hold back the kernels that read a peer's bytes.  Every wait is bounded by
-// `limit` wall-clock ticks: on expiry the lane sets *err and returns, so the grid
-// always drains (the host turns *err into an error after the stream synchronises).
-// ---------------------------------------------------------------------------------
-constexpr int kMaxSig = 64;
-
-struct SigArgs {
-    uint64_t *waddr[kMaxSig];
-    uint64_t wval[kMaxSig];
-    const uint64_t *qaddr[kMaxSig];
-    uint64_t qval[kMaxSig];
-    uint64_t *err;
-    long long limit;
-    int nw, nq;
-};
-
-__global__ __launch_bounds__(kMaxSig) void k_p2p_signal(SigArgs a)
-{
-    const int i = threadIdx.x;
-    if (i < a.nw) __hip_atomic_store(a.waddr[i], a.wval[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    __syncthreads();
-    if (i < a.nq) {
-        const long long t0 = wall_clock64();
-        while (__hip_atomic_load(a.qaddr[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.qval[i]) {
-            if (wall_clock64() - t0 > a.limit) {
-                __hip_atomic_store(a.err, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-}
-
 }  // namespace sos
 
 using namespace sos;
 
-extern "C" {
+namespace {
 
-// Copy nseg (src, dst, bytes) segments in one launch (<= 16 per launch; more are
-// split into several launches).  src may be peer memory mapped by IPC.
-int sosx_gather(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,
-                void *stream)
+// A gate's signalling step as its own one-workgroup launch.
+int launch_step(const Sig<kMaxGate> &gate, hipStream_t st)
 {
-    hipStream_t st = as_stream(stream);
+    SigArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int i = 0; i < gate.nw; ++i) {
+        a.waddr[i] = gate.waddr[i];
+        a.wval[i] = gate.wval[i];
+    }
+    for (int i = 0; i < gate.nq; ++i) {
+        a.qaddr[i] = gate.qaddr[i];
+        a.qval[i] = gate.qval[i];
+    }
+    a.nw = gate.nw;
+    a.nq = gate.nq;
+    a.err = gate.err;
+    a.limit = gate.limit;
+    hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(kMaxSig), 0, st, a);
+    return hip_ok(hipGetLastError());
+}
+
+// Copy nseg (src, dst, bytes) segments, <= 16 per launch.  `gate` (or null): a signalling
+// step that must precede the copies -- carried by the first launch when its grid is
+// small enough, else run by its own k_p2p_signal launch first.
+int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,
+                const Sig<kMaxGate> *gate, hipStream_t st)
+{
+    bool gate_pending = gate != nullptr;
     for (int base = 0; base < nseg; base += kMaxSeg) {
         GatherArgs g;
         memset(&g, 0, sizeof(g));
@@ -126,10 +165,59 @@ int sosx_gather(int nseg, const void *const *srcs, void *const *dsts, const size
         uint64_t blocks = (tot + kThreads * 4 - 1) / (kThreads * 4);
         if (blocks < 1) blocks = 1;
         if (blocks > 16384) blocks = 16384;
-        hipLaunchKernelGGL(k_gather, dim3((unsigned)blocks), dim3(kThreads), 0, st, g);
+        Sig<kMaxGate> none;
+        memset(&none, 0, sizeof(none));
+        if (gate_pending && blocks <= kGateMaxBlocks) {
+            hipLaunchKernelGGL(k_gather<true>, dim3((unsigned)blocks), dim3(kThreads), 0, st, g, *gate);
+            gate_pending = false;
+        } else {
+            if (gate_pending) {  // large grid: the step as its own launch
+                if (launch_step(*gate, st) != SOSX_OK) return SOSX_ERR_HIP;
+                gate_pending = false;
+            }
+            hipLaunchKernelGGL(k_gather<false>, dim3((unsigned)blocks), dim3(kThreads), 0, st, g, none);
+        }
         if (hipGetLastError() != hipSuccess) return SOSX_ERR_HIP;
     }
+    if (gate_pending && launch_step(*gate, st) != SOSX_OK) return SOSX_ERR_HIP;  // nothing copied
     return SOSX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Copy nseg (src, dst, bytes) segments in one launch (<= 16 per launch; more are
+// split into several launches).  src may be peer memory mapped by IPC.
+int sosx_gather(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,
+                void *stream)
+{
+    return gather_impl(nseg, srcs, dsts, bytes, nullptr, as_stream(stream));
+}
+
+// sosx_gather preceded by a p2p signalling step (the arguments of sosx_p2p_signal, at
+// most 16 stores and 16 waits): small grids carry the step in the copy launch itself.
+int sosx_gather_signalled(int nseg, const void *const *srcs, void *const *dsts,
+                          const size_t *bytes, int nw, uint64_t *const *waddr,
+                          const uint64_t *wval, int nq, const uint64_t *const *qaddr,
+                          const uint64_t *qval, uint64_t *err, long long limit_ticks, void *stream)
+{
+    if (nw < 0 || nq < 0 || nw > kMaxGate || nq > kMaxGate || (nq && !err)) return SOSX_ERR_ARG;
+    Sig<kMaxGate> gate;
+    memset(&gate, 0, sizeof(gate));
+    for (int i = 0; i < nw; ++i) {
+        gate.waddr[i] = waddr[i];
+        gate.wval[i] = wval[i];
+    }
+    for (int i = 0; i < nq; ++i) {
+        gate.qaddr[i] = qaddr[i];
+        gate.qval[i] = qval[i];
+    }
+    gate.nw = nw;
+    gate.nq = nq;
+    gate.err = err;
+    gate.limit = limit_ticks;
+    return gather_impl(nseg, srcs, dsts, bytes, &gate, as_stream(stream));
 }
 
 // One signalling step of the p2p transport on `stream`: store vals[i] to waddr[i]

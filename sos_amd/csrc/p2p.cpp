@@ -403,6 +403,7 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
             }
         }
         int rc;
+        bool step_pending = false;  // the signalling step still to be enqueued
         if (first_xfer_round) {
             // the call's entry boundary runs on the host, as in host mode: nothing is
             // queued ahead of it that a signal kernel could overlap (stream sync only
@@ -413,8 +414,7 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
             if (sends && hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
             host_flush();
         } else {
-            rc = flush();
-            if (rc) return rc;
+            step_pending = true;
         }
         struct Seg { const char *src; char *dst; uint64_t bytes; bool used; };
         std::vector<Seg> segs;
@@ -456,11 +456,40 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
                 gd.push_back(sg.dst);
                 gb.push_back(sg.bytes);
             }
-        if (!gs.empty()) {
+        if (step_pending && !gs.empty() && pw_store.size() <= 16 && pw_wait.size() <= 16) {
+            // the step rides in the gather launch (small grids; else its own launch)
+            std::vector<uint64_t *> wa;
+            std::vector<uint64_t> wv;
+            std::vector<const uint64_t *> qa;
+            std::vector<uint64_t> qv;
+            for (auto &kv : pw_store) {
+                wa.push_back(dev(kv.first));
+                wv.push_back(kv.second);
+            }
+            for (auto &kv : pw_wait) {
+                qa.push_back(dev(kv.first));
+                qv.push_back(kv.second);
+            }
+            pw_store.clear();
+            pw_wait.clear();
             prof_mark(1, false, stream);
-            rc = sosx_gather((int)gs.size(), gs.data(), gd.data(), gb.data(), stream);
+            rc = sosx_gather_signalled((int)gs.size(), gs.data(), gd.data(), gb.data(),
+                                       (int)wa.size(), wa.data(), wv.data(), (int)qa.size(),
+                                       qa.data(), qv.data(), dev(&sh->sig_err[my_world]),
+                                       g_sig.limit_ticks, stream);
             prof_mark(1, true, stream);
             if (rc) return rc;
+        } else {
+            if (step_pending) {
+                rc = flush();
+                if (rc) return rc;
+            }
+            if (!gs.empty()) {
+                prof_mark(1, false, stream);
+                rc = sosx_gather((int)gs.size(), gs.data(), gd.data(), gb.data(), stream);
+                prof_mark(1, true, stream);
+                if (rc) return rc;
+            }
         }
         if (fuse_ok) {
             rc = run_round_ops(r, ins, local_ptr, op, dt, stream);
