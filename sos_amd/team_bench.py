@@ -42,9 +42,15 @@ TRANSPORTS = (("rccl", 0, None, 0), ("rccl_ag", 0, None, 1), ("p2p", 1, 1, 0),
               ("p2p_host", 1, 0, 0))
 T_NAMES = tuple(t[0] for t in TRANSPORTS)
 
+# transports that failed the preflight on some rank (every leg skips them)
+DISABLED = set()
+PREFLIGHT_PORT_OFFSET = 11   # the preflight job bootstraps on MASTER_PORT + 12
+
 
 def use_transport(S, L, tname):
     """Switch every PE (collectively) to `tname`; False when it is unavailable."""
+    if tname in DISABLED:
+        return False
     _, tid, sig, ag = next(t for t in TRANSPORTS if t[0] == tname)
     if S.lib().shmemx_set_transport(tid) < 0:
         return False
@@ -74,6 +80,7 @@ def main(args, torch):
     dt = L.dtype_id(args.dtype)
     es = L.dtype_size(dt)
     n = args.n
+    user_transport = os.environ.get("SHMEMX_TRANSPORT")
     os.environ.setdefault("SHMEMX_TRANSPORT", "both")
     sweep_sizes = [] if getattr(args, "no_team_sweep", False) else \
         [m for m in (1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20)
@@ -88,6 +95,16 @@ def main(args, torch):
     os.environ.setdefault("SHMEMX_P2P_TIMEOUT", "120")
     os.environ.setdefault("SHMEM_SYMMETRIC_SIZE", str(2 * (16 << 20) * es + (64 << 20)))
     dist.init_process_group("gloo")
+    pre = preflight(torch, dist, rank, world)
+    DISABLED.update(k for k, ok in pre["ok"].items() if not ok)
+    if user_transport is None:
+        # a transport that failed everywhere is not even brought up in this job
+        p2p_any = pre["ok"]["p2p"] or pre["ok"]["p2p_host"]
+        rccl_any = pre["ok"]["rccl"] or pre["ok"]["rccl_ag"]
+        if p2p_any != rccl_any:
+            os.environ["SHMEMX_TRANSPORT"] = "p2p" if p2p_any else "rccl"
+    if rank == 0 and DISABLED:
+        log(f"[team] preflight: transports {sorted(DISABLED)} disabled ({pre['why']})")
     S.shmem_init()
     assert S.shmem_n_pes() == world and S.shmem_my_pe() == rank
     alg = L.ALGS[args.alg]
@@ -114,7 +131,7 @@ def main(args, torch):
         log(f"[team] {world} PEs, nreduce {n}, alg {name}: heap {os.environ['SHMEMX_DEVICE_HEAP_SIZE']} B")
     for tid, tname in enumerate(T_NAMES):
         if not use_transport(S, L, tname):
-            results[tname] = {"available": False}
+            results[tname] = {"available": False, "preflight_failed": tname in DISABLED}
             continue
         if rank == 0:
             log(f"[team] {tname}: warmup + {args.steps} timed steps")
@@ -234,6 +251,7 @@ def main(args, torch):
                                "(SHMEMX_TRANSPORT selects; rccl_ag = rccl with "
                                "SHMEMX_RCCL_ALLGATHER=1, p2p_host = p2p with "
                                "SHMEMX_P2P_SIGNAL=host)")
+    res["preflight"] = pre
     if curve:
         res["size_curve"] = curve
     if schedules:
@@ -615,3 +633,103 @@ def self_check(torch, L, S, dt, opid, dist_kind, seed, world, n, es, alg, dst, s
     bad = L.count_mismatch(exp.data_ptr(), dst, n, es, stream)
     del ins
     return bad
+
+
+def preflight(torch, dist, rank, world):
+    """Run every transport once in a short-lived child PE job before the bench brings
+    them up in this one.  A transport that hangs, times out (the p2p waits end the process
+    with _exit) or returns wrong bytes there is disabled on every rank here, so that one
+    broken transport cannot take the whole N > 1 line with it.  The child job is the same
+    library and the same torchrun ranks, bootstrapped on MASTER_PORT + 12, with the p2p
+    wait bound at 20 s; its results are agreed over gloo (a transport counts only when
+    it passed on every rank).  SOSX_BENCH_PREFLIGHT=0 skips it."""
+    import subprocess
+    ok = {k: True for k in T_NAMES}
+    if os.environ.get("SOSX_BENCH_PREFLIGHT", "1") == "0":
+        return {"ran": False, "ok": ok, "why": "SOSX_BENCH_PREFLIGHT=0"}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.update(MASTER_PORT=str(int(os.environ["MASTER_PORT"]) + PREFLIGHT_PORT_OFFSET),
+               SHMEMX_TRANSPORT=os.environ.get("SHMEMX_TRANSPORT", "both"),
+               SHMEMX_P2P_TIMEOUT="20", SHMEM_BOOTSTRAP_TIMEOUT="60",
+               SHMEMX_DEVICE_HEAP_SIZE=str(512 << 20), SHMEMX_STAGE_BYTES=str(64 << 20),
+               SHMEM_SYMMETRIC_SIZE=str(64 << 20))
+    t0 = time.perf_counter()
+    why = ""
+    try:
+        cp = subprocess.run([sys.executable, "-u", "-m", "sos_amd.team_bench", "--preflight"],
+                            cwd=root, env=env, capture_output=True, text=True, timeout=240)
+        out, err, rc = cp.stdout, cp.stderr, cp.returncode
+    except subprocess.TimeoutExpired as e:
+        out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
+        err = e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
+        rc, why = -9, "child timed out"
+    seen = {}
+    for line in out.splitlines():
+        if line.startswith("{"):
+            try:
+                d = json.loads(line)
+            except ValueError:
+                continue
+            if d.get("t") in ok:
+                seen[d["t"]] = bool(d.get("ok"))
+    for k in T_NAMES:       # a transport the child never reported (it died first) failed
+        ok[k] = seen.get(k, False)
+    if rc != 0 and not why:
+        why = f"child rc={rc}"
+    if rc != 0 or not all(ok.values()):
+        tail = "\n".join((err or "").strip().splitlines()[-6:])
+        log(f"[team] rank {rank} preflight: {seen} ({why or 'check failed'})\n{tail}")
+    flags = torch.tensor([1 if ok[k] else 0 for k in T_NAMES], dtype=torch.int64)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    agreed = {k: bool(v) for k, v in zip(T_NAMES, flags.tolist())}
+    return {"ran": True, "ok": agreed, "seconds": round(time.perf_counter() - t0, 1),
+            "why": why or ("ok" if all(agreed.values()) else "bitwise check or availability")}
+
+
+def preflight_child():
+    """The preflight job (one PE per torchrun rank): each transport in turn runs a
+    recdbl-sized (1Ki) and a ring-sized (4Mi) float sum reduce on fresh inputs, checked
+    bit for bit; one JSON line per transport as soon as it is done."""
+    import torch
+    from sos_amd import _lib as L
+    from sos_amd import shmem as S
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank)) % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local)
+    os.environ.setdefault("SHMEMX_DEVICE", str(local))
+    S.shmem_init()
+    dt = L.dtype_id("float")
+    es = L.dtype_size(dt)
+    stream = S.lib().shmemx_get_stream()
+    nmax = 4 << 20
+    src = S.shmemx_malloc_device(nmax * es)
+    dst = S.shmemx_malloc_device(nmax * es)
+    team = S.team_world()
+    alg = L.ALGS["auto"]
+    S.shmemx_set_reduce_algorithm(alg)
+    for tid, tname in enumerate(T_NAMES):
+        if not use_transport(S, L, tname):
+            print(json.dumps({"t": tname, "ok": False, "why": "unavailable"}), flush=True)
+            continue
+        bad = 0
+        for k, n in enumerate((1024, nmax)):
+            seed = 0x9F1E + 16 * tid + k
+            L.fill(dt, L.DIST_UNIFORM, seed, rank, src, n, 0, stream)
+            torch.cuda.synchronize()
+            S.shmem_barrier_all()
+            S.shmem_float_sum_reduce(team, dst, src, n)
+            bad += self_check(torch, L, S, dt, L.op_id("sum"), L.DIST_UNIFORM, seed, world, n,
+                              es, alg, dst, stream)
+        S.shmem_barrier_all()
+        print(json.dumps({"t": tname, "ok": bad == 0, "mismatches": bad}), flush=True)
+    reset_transport(S, L)
+    S.shmemx_free_device(dst)
+    S.shmemx_free_device(src)
+    S.shmem_finalize()
+    return 0
+
+
+if __name__ == "__main__" and "--preflight" in sys.argv:
+    sys.exit(preflight_child())

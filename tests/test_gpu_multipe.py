@@ -214,9 +214,10 @@ def test_team_check_host_stripes(np_, signal):
 
 def test_bench_team_leg_default_transport():
     """bench.py's N > 1 default (SHMEMX_TRANSPORT=both, what the driver's 8-GPU run uses),
-    here with 2 ranks on one GPU: RCCL refuses a second rank on the device, so init falls
-    back -- on every PE, agreed over the bootstrap -- to the p2p transport, and the line
-    comes out with clean checks."""
+    here with 2 ranks on one GPU: RCCL refuses a second rank on the device, so in the
+    preflight job init falls back -- on every PE, agreed over the bootstrap -- to the p2p
+    transport; the bench job then brings up p2p only, and the line comes out with clean
+    checks."""
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
               "SHMEMX_TRANSPORT"):
@@ -235,4 +236,8 @@ def test_bench_team_leg_default_transport():
     assert res["config"]["transport"] in ("p2p", "p2p_host")
     assert list(res["transports"]) == ["p2p", "p2p_host"]
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0
-    assert "every PE runs on the p2p transport" in r.stderr
+    # the preflight job found RCCL down (init refused, every PE fell back) and p2p clean,
+    # so this job brought up p2p only
+    assert res["preflight"]["ran"] and res["preflight"]["ok"] == \
+        {"rccl": False, "rccl_ag": False, "p2p": True, "p2p_host": True}, res["preflight"]
+    assert "preflight: transports ['rccl', 'rccl_ag'] disabled" in r.stderr

@@ -48,3 +48,71 @@ def test_unavailable_transports_report_false():
     lib = _Lib({1}, stream_ok=False)   # RCCL down, stream signalling unavailable
     S = L = _Wrap(lib)
     assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [False, False, False, True]
+
+
+class _Dist:
+    """gloo stand-in for one rank: all_reduce(MIN) leaves the tensor as it is."""
+    class ReduceOp:
+        MIN = "min"
+
+    def all_reduce(self, t, op=None):
+        assert op == "min"
+
+
+def _run_preflight(monkeypatch, stdout, rc=0, timeout=False):
+    import subprocess
+    import torch
+
+    def fake_run(cmd, **kw):
+        assert cmd[-3:] == ["-m", "sos_amd.team_bench", "--preflight"]
+        env = kw["env"]
+        assert env["MASTER_PORT"] == str(29500 + TB.PREFLIGHT_PORT_OFFSET)
+        assert env["SHMEMX_P2P_TIMEOUT"] == "20"
+        if timeout:
+            raise subprocess.TimeoutExpired(cmd, kw["timeout"], output=stdout.encode(), stderr=b"")
+        return subprocess.CompletedProcess(cmd, rc, stdout, "")
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    monkeypatch.delenv("SOSX_BENCH_PREFLIGHT", raising=False)
+    return TB.preflight(torch, _Dist(), 0, 2)
+
+
+def test_preflight_all_clean(monkeypatch):
+    out = "".join(f'{{"t": "{t}", "ok": true}}\n' for t in TB.T_NAMES)
+    pre = _run_preflight(monkeypatch, out)
+    assert pre["ran"] and all(pre["ok"].values()) and pre["why"] == "ok"
+
+
+def test_preflight_child_died_mid_way(monkeypatch):
+    """The child ended (a p2p wait's _exit) after reporting rccl/rccl_ag: the transport it
+    died in and every one it never reached count as failed."""
+    out = 'noise\n{"t": "rccl", "ok": true}\n{"t": "rccl_ag", "ok": true}\n'
+    pre = _run_preflight(monkeypatch, out, rc=1)
+    assert pre["ok"] == {"rccl": True, "rccl_ag": True, "p2p": False, "p2p_host": False}
+    assert pre["why"] == "child rc=1"
+
+
+def test_preflight_mismatch_and_timeout(monkeypatch):
+    out = ('{"t": "rccl", "ok": true}\n{"t": "rccl_ag", "ok": false, "mismatches": 3}\n'
+           '{"t": "p2p", "ok": true}\n')
+    pre = _run_preflight(monkeypatch, out, timeout=True)
+    assert pre["ok"] == {"rccl": True, "rccl_ag": False, "p2p": True, "p2p_host": False}
+    assert pre["why"] == "child timed out"
+
+
+def test_preflight_disabled_transports_are_skipped():
+    lib = _Lib({0, 1}, stream_ok=True)
+    S = L = _Wrap(lib)
+    TB.DISABLED.update({"p2p", "rccl_ag"})
+    try:
+        assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [True, False, False, True]
+    finally:
+        TB.DISABLED.clear()
+
+
+def test_preflight_off(monkeypatch):
+    import torch
+    monkeypatch.setenv("SOSX_BENCH_PREFLIGHT", "0")
+    pre = TB.preflight(torch, _Dist(), 0, 2)
+    assert not pre["ran"] and all(pre["ok"].values())
