@@ -45,6 +45,7 @@ T_NAMES = tuple(t[0] for t in TRANSPORTS)
 # transports that failed the preflight on some rank (every leg skips them)
 DISABLED = set()
 PREFLIGHT_PORT_OFFSET = 11   # the preflight job bootstraps on MASTER_PORT + 12
+PREFLIGHT_LIMIT_S = 150.0    # the preflight job is killed after this long
 
 
 def use_transport(S, L, tname):
@@ -642,7 +643,8 @@ def preflight(torch, dist, rank, world):
     broken transport cannot take the whole N > 1 line with it.  The child job is the same
     library and the same torchrun ranks, bootstrapped on MASTER_PORT + 12, with the p2p
     wait bound at 20 s; its results are agreed over gloo (a transport counts only when
-    it passed on every rank).  SOSX_BENCH_PREFLIGHT=0 skips it."""
+    it passed on every rank).  The child is killed after PREFLIGHT_LIMIT_S (a transport
+    that hangs without a bound, e.g. in RCCL init).  SOSX_BENCH_PREFLIGHT=0 skips it."""
     import subprocess
     ok = {k: True for k in T_NAMES}
     if os.environ.get("SOSX_BENCH_PREFLIGHT", "1") == "0":
@@ -656,14 +658,27 @@ def preflight(torch, dist, rank, world):
                SHMEM_SYMMETRIC_SIZE=str(64 << 20))
     t0 = time.perf_counter()
     why = ""
-    try:
-        cp = subprocess.run([sys.executable, "-u", "-m", "sos_amd.team_bench", "--preflight"],
-                            cwd=root, env=env, capture_output=True, text=True, timeout=240)
-        out, err, rc = cp.stdout, cp.stderr, cp.returncode
-    except subprocess.TimeoutExpired as e:
-        out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
-        err = e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
-        rc, why = -9, "child timed out"
+    import tempfile
+    with tempfile.TemporaryFile("w+") as fo, tempfile.TemporaryFile("w+") as fe:
+        child = subprocess.Popen([sys.executable, "-u", "-m", "sos_amd.team_bench", "--preflight"],
+                                 cwd=root, env=env, stdout=fo, stderr=fe)
+        next_note = 20.0
+        while child.poll() is None:
+            el = time.perf_counter() - t0
+            if el > PREFLIGHT_LIMIT_S:
+                child.kill()
+                child.wait()
+                why = f"child killed after {PREFLIGHT_LIMIT_S:.0f} s"
+                break
+            if el > next_note:      # progress lines: a silent wait looks like a hang
+                if rank == 0:
+                    log(f"[team] preflight job still running ({el:.0f} s)")
+                next_note += 20.0
+            time.sleep(0.2)
+        rc = child.returncode
+        fo.seek(0)
+        fe.seek(0)
+        out, err = fo.read(), fe.read()
     seen = {}
     for line in out.splitlines():
         if line.startswith("{"):
@@ -709,7 +724,12 @@ def preflight_child():
     team = S.team_world()
     alg = L.ALGS["auto"]
     S.shmemx_set_reduce_algorithm(alg)
+    # test hook (tests/test_gpu_fakerccl.py): SOSX_PREFLIGHT_FAULT=<transport>:<rank> makes
+    # that rank vanish when it reaches that transport, so its peers meet a real p2p timeout
+    fault_t, _, fault_r = os.environ.get("SOSX_PREFLIGHT_FAULT", "").partition(":")
     for tid, tname in enumerate(T_NAMES):
+        if tname == fault_t and fault_r and int(fault_r) == rank:
+            os._exit(0)
         if not use_transport(S, L, tname):
             print(json.dumps({"t": tname, "ok": False, "why": "unavailable"}), flush=True)
             continue
@@ -718,11 +738,9 @@ def preflight_child():
             seed = 0x9F1E + 16 * tid + k
             L.fill(dt, L.DIST_UNIFORM, seed, rank, src, n, 0, stream)
             torch.cuda.synchronize()
-            S.shmem_barrier_all()
             S.shmem_float_sum_reduce(team, dst, src, n)
             bad += self_check(torch, L, S, dt, L.op_id("sum"), L.DIST_UNIFORM, seed, world, n,
                               es, alg, dst, stream)
-        S.shmem_barrier_all()
         print(json.dumps({"t": tname, "ok": bad == 0, "mismatches": bad}), flush=True)
     reset_transport(S, L)
     S.shmemx_free_device(dst)

@@ -132,6 +132,32 @@ def test_bench_team_leg_rccl():
         assert curve[-1]["bitwise_mismatches_all_ranks"] == 0   # 4Mi: equal chunks
 
 
+def test_bench_preflight_drops_a_hanging_transport():
+    """The N > 1 bench's preflight against a transport that hangs: both transports are up
+    (SHMEMX_TRANSPORT=both, RCCL through the stand-in), and in the preflight job PE 1
+    vanishes when it reaches p2p, so PE 0's p2p call meets the real bounded wait (20 s in
+    the preflight) and ends that process.  The bench job must then bring up RCCL only and
+    print a clean line from both RCCL variants."""
+    env = _env()
+    env["SOSX_PREFLIGHT_FAULT"] = "p2p:1"
+    env.pop("SHMEMX_TRANSPORT")   # the bench's own default (both), as the driver runs it
+    port = 29100 + os.getpid() % 500
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu",
+                        "--nreduce", str((1 << 20) + 3), "--sweep-max", str(4 << 20)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["preflight"]["ok"] == {"rccl": True, "rccl_ag": True, "p2p": False,
+                                      "p2p_host": False}, res["preflight"]
+    assert "timed out" in r.stderr, r.stderr[-3000:]
+    assert list(res["transports"]) == ["rccl", "rccl_ag"], res["transports"]
+    assert res["config"]["transport"] in ("rccl", "rccl_ag")
+    assert res["check"]["bitwise_mismatches_all_ranks"] == 0, res["check"]
+
+
 @pytest.mark.parametrize("script", ["team_check.py", "team_mgmt_check.py"])
 def test_init_attr_multi_pe(tmp_path, script, np_=3):
     """shmemx_init_attr across 3 processes (unique id passed out of band, no bootstrap hub):

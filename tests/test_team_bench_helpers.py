@@ -63,16 +63,31 @@ def _run_preflight(monkeypatch, stdout, rc=0, timeout=False):
     import subprocess
     import torch
 
-    def fake_run(cmd, **kw):
-        assert cmd[-3:] == ["-m", "sos_amd.team_bench", "--preflight"]
-        env = kw["env"]
-        assert env["MASTER_PORT"] == str(29500 + TB.PREFLIGHT_PORT_OFFSET)
-        assert env["SHMEMX_P2P_TIMEOUT"] == "20"
-        if timeout:
-            raise subprocess.TimeoutExpired(cmd, kw["timeout"], output=stdout.encode(), stderr=b"")
-        return subprocess.CompletedProcess(cmd, rc, stdout, "")
+    class FakePopen:
+        def __init__(self, cmd, cwd=None, env=None, stdout=None, stderr=None):
+            assert cmd[-3:] == ["-m", "sos_amd.team_bench", "--preflight"]
+            assert env["MASTER_PORT"] == str(29500 + TB.PREFLIGHT_PORT_OFFSET)
+            assert env["SHMEMX_P2P_TIMEOUT"] == "20"
+            stdout.write(out_text)
+            stdout.flush()
+            self.returncode = None
+            self.killed = False
 
-    monkeypatch.setattr(subprocess, "run", fake_run)
+        def poll(self):
+            if not timeout:
+                self.returncode = rc
+            return self.returncode
+
+        def kill(self):
+            self.killed = True
+            self.returncode = -9
+
+        def wait(self):
+            return self.returncode
+
+    out_text = stdout
+    monkeypatch.setattr(subprocess, "Popen", FakePopen)
+    monkeypatch.setattr(TB, "PREFLIGHT_LIMIT_S", 0.5)
     monkeypatch.setenv("MASTER_PORT", "29500")
     monkeypatch.delenv("SOSX_BENCH_PREFLIGHT", raising=False)
     return TB.preflight(torch, _Dist(), 0, 2)
@@ -98,7 +113,7 @@ def test_preflight_mismatch_and_timeout(monkeypatch):
            '{"t": "p2p", "ok": true}\n')
     pre = _run_preflight(monkeypatch, out, timeout=True)
     assert pre["ok"] == {"rccl": True, "rccl_ag": False, "p2p": True, "p2p_host": False}
-    assert pre["why"] == "child timed out"
+    assert pre["why"] == "child killed after 0 s"
 
 
 def test_preflight_disabled_transports_are_skipped():
