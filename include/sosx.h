@@ -183,6 +183,14 @@ int sosx_set_p2p_signal_mode(int mode);
  * start value).  Collective switch; returns the previous setting. */
 int sosx_set_rccl_allgather(int on);
 
+/* RCCL executor: reductions over a world-shaped team as one ncclAllReduce where RCCL has
+ * the type and op.  0 = off (default; every call runs its SOS schedule), 1 = integer
+ * sum/prod/min/max of 8/32/64-bit types (two's-complement results are the same in any
+ * order, so bit-exact), 2 = also float/double sum/prod (RCCL's order: within the fp
+ * tolerance, not bit-exact with SOS's ring).  SHMEMX_RCCL_ALLREDUCE sets the start
+ * value.  Collective switch; returns the previous mode, -1 if out of range. */
+int sosx_set_rccl_allreduce(int mode);
+
 /* Kernel variant selection for the hot fp32/generic combine (bench/tuning only):
  * returns the previous variant.  0 = default. */
 int sosx_set_combine_variant(int variant);

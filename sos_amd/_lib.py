@@ -84,6 +84,7 @@ _SIGS = {
     "sosx_p2p_signal_mode": (_c.c_int, []),
     "sosx_set_p2p_signal_mode": (_c.c_int, [_c.c_int]),
     "sosx_set_rccl_allgather": (_c.c_int, [_c.c_int]),
+    "sosx_set_rccl_allreduce": (_c.c_int, [_c.c_int]),
 }
 
 

@@ -205,6 +205,42 @@ int exec_rccl(const Plan &p, const Team &t, const Bufs &b, int op, int dt, hipSt
     return SOSX_OK;
 }
 
+// SHMEMX_RCCL_ALLREDUCE (sosx_set_rccl_allreduce): may this reduction run as one
+// ncclAllReduce?  Only over a world-shaped team (the communicator is the world's) and
+// only where RCCL's type and op give the combine's own element semantics: integer
+// sum/prod/min/max of 8/32/64-bit kinds (dtypes.h: char, ptrdiff_t and the unsigned
+// types included) are the same in any order -- two's-complement wrap, min/max with the
+// kind's signedness -- so mode 1 stays bit-exact; mode 2 adds fp32/fp64 sum/prod, whose
+// bits follow RCCL's order instead of SOS's (DESIGN.md section 5 tolerance).  No RCCL
+// type for 16-bit integers, no bitwise ops, no complex or long double: those keep their
+// SOS schedule.
+bool rccl_allreduce_type(const Team &t, int op, int dt, ncclDataType_t *ty, ncclRedOp_t *ro)
+{
+    const State &s = st();
+    if (!s.rccl_allreduce || !s.comm || s.transport != TRANSPORT_RCCL || t.start != 0 ||
+        t.stride != 1 || t.size != s.n_pes)
+        return false;
+    switch (op) {
+        case SOSX_OP_SUM: *ro = ncclSum; break;
+        case SOSX_OP_PROD: *ro = ncclProd; break;
+        case SOSX_OP_MIN: *ro = ncclMin; break;
+        case SOSX_OP_MAX: *ro = ncclMax; break;
+        default: return false;
+    }
+    const bool fp_ok = s.rccl_allreduce >= 2 && (op == SOSX_OP_SUM || op == SOSX_OP_PROD);
+    switch (sos_dtype_info(dt).kind) {
+        case K_S8: *ty = ncclInt8; return true;
+        case K_U8: *ty = ncclUint8; return true;
+        case K_S32: *ty = ncclInt32; return true;
+        case K_U32: *ty = ncclUint32; return true;
+        case K_S64: *ty = ncclInt64; return true;
+        case K_U64: *ty = ncclUint64; return true;
+        case K_F32: *ty = ncclFloat32; return fp_ok;
+        case K_F64: *ty = ncclFloat64; return fp_ok;
+        default: return false;
+    }
+}
+
 // Plan cache: the same call shape every step reuses its plan.
 const Plan &cached_plan(int alg, int P, int me, uint64_t count, uint64_t ts, unsigned smis,
                         unsigned dmis)
@@ -418,14 +454,18 @@ bool striped_host_ring(int alg, void *target, const void *source, size_t count, 
 }
 
 // Run plan `alg` (a reduction SOSX_ALG_*, a scan or a broadcast, plan.h) for this PE
-// over team t, on the library stream; returns when the call is complete.
+// over team t, on the library stream; returns when the call is complete.  `reduction`:
+// the call may take the ncclAllReduce path (rccl_allreduce_type).
 void execute(int alg, void *target, const void *source, size_t count, size_t ts, const Team &t,
-             int op, int dt, const char *fn)
+             int op, int dt, const char *fn, bool reduction = false)
 {
     State &s = st();
     const size_t bytes = count * ts;
     int rc;
-    if (striped_host_ring(alg, target, source, count, ts, t, op, dt, fn)) return;
+    ncclDataType_t ar_ty = ncclUint8;
+    ncclRedOp_t ar_op = ncclSum;
+    const bool ar = reduction && rccl_allreduce_type(t, op, dt, &ar_ty, &ar_op);
+    if (!ar && striped_host_ring(alg, target, source, count, ts, t, op, dt, fn)) return;
     if (s.transport == TRANSPORT_P2P) {
         // buffers must live in the IPC-mapped device heap; anything else is staged
         // through this PE's stage region (in place), whose offset is published
@@ -468,6 +508,21 @@ void execute(int alg, void *target, const void *source, size_t count, size_t ts,
         if (!dev_src) dsrc = stg;
         if (!dev_dst) ddst = target == source ? stg : stg + half;
     }
+    if (ar) {
+        if (!dev_src) hip_check(hipMemcpyAsync(stg, source, bytes, hipMemcpyHostToDevice, s.stream), "H2D");
+        if (g_prof.on) {
+            g_prof.ncall++;
+            (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, false), s.stream);
+        }
+        if (ncclAllReduce(dsrc, ddst, count, ar_ty, ar_op, s.comm, s.stream) != ncclSuccess)
+            raise_error("%s: %s", fn, status_text(SOSX_ERR_RCCL));
+        if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, true), s.stream);
+        if (!dev_dst)
+            hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
+        hip_check(hipStreamSynchronize(s.stream), fn);
+        if (g_prof.on) g_prof.collect();
+        return;
+    }
     const Plan &p = cached_plan(alg, t.size, t.my_idx, count, ts, (unsigned)((uintptr_t)dsrc & 15),
                                 (unsigned)((uintptr_t)ddst & 15));
     if (!dev_src && p.reads_src)
@@ -502,7 +557,7 @@ void op_to_all(void *target, const void *source, size_t count, size_t ts, const 
     int alg = sosplan::resolve_alg(s.reduce_alg, bytes, s.coll_size_crossover);
     if ((alg == SOSX_ALG_RING || alg == SOSX_ALG_RECDBL_DIRECT) && t.size > SOSX_MAX_FOLD)
         alg = SOSX_ALG_RECHALVING;
-    execute(alg, target, source, count, ts, t, op, dt, fn);
+    execute(alg, target, source, count, ts, t, op, dt, fn, true);
 }
 
 // SHMEM_ERR_CHECK_OVERLAP (src/shmem_internal.h:319-336), complete overlap allowed

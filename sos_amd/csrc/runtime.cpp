@@ -161,6 +161,8 @@ static void read_env(State &s)
     s.sym_stage_bytes = atol_scaled(getenv("SHMEMX_STAGE_BYTES"), 512ull << 20);
     const char *ag = getenv("SHMEMX_RCCL_ALLGATHER");
     s.rccl_allgather = ag && atoi(ag) != 0;
+    const char *ar = getenv("SHMEMX_RCCL_ALLREDUCE");
+    s.rccl_allreduce = ar ? std::min(std::max(atoi(ar), 0), 2) : 0;
     s.sym_stage_bytes = (s.sym_stage_bytes + 4095) & ~(size_t)4095;
     if (s.sym_stage_bytes >= s.dev_heap_bytes) s.dev_heap_bytes = s.sym_stage_bytes + (256u << 20);
 }
@@ -823,6 +825,19 @@ int sosx_set_rccl_allgather(int on)
     State &s = st();
     const int prev = s.rccl_allgather ? 1 : 0;
     s.rccl_allgather = on != 0;
+    return prev;
+}
+
+// RCCL executor: world-team reductions as one ncclAllReduce where RCCL has the type and
+// op (0 off, the default; 1 integer sum/prod/min/max, bit-exact; 2 also fp32/fp64
+// sum/prod, within the fp tolerance of DESIGN.md section 5).  Collective; returns the
+// previous mode, or -1 for a mode out of range.
+int sosx_set_rccl_allreduce(int mode)
+{
+    State &s = st();
+    if (mode < 0 || mode > 2) return -1;
+    const int prev = s.rccl_allreduce;
+    s.rccl_allreduce = mode;
     return prev;
 }
 

@@ -100,6 +100,9 @@ struct State {
     int transport = TRANSPORT_RCCL;   // the transport calls use now
     bool rccl_allgather = false;      // SHMEMX_RCCL_ALLGATHER: equal-chunk allgather rounds
                                       // of a world-team plan as one ncclAllGather
+    int rccl_allreduce = 0;           // SHMEMX_RCCL_ALLREDUCE: world-team reductions as one
+                                      // ncclAllReduce: 1 integer sum/prod/min/max (bit-exact
+                                      // in any order), 2 also fp32/fp64 sum/prod (tolerance)
     bool want_rccl = true;            // create the RCCL communicator
     bool want_p2p = false;            // IPC-map the device heap on every PE
     bool p2p_ready = false;           // heap mapped (or single PE)

@@ -12,6 +12,9 @@ Both inter-PE transports are measured (SHMEMX_TRANSPORT=both):
                HBM; stream-ordered signals between rounds (one host sync per call)
   rccl_ag    : the same, the allgather round as one ncclAllGather when chunks are equal
   p2p_host   : p2p with the host moving the transfer counters every round
+  rccl_ar    : RCCL's own ncclAllReduce (SHMEMX_RCCL_ALLREDUCE=2): the reference point
+               for the SOS schedules; for fp sum its bits follow RCCL's order, so it is
+               checked against the fp tolerance bound instead and never gives `value`
 `value` is the fastest one whose bitwise check is clean.
 Self-check: after timing, every rank regenerates all P inputs on its own GPU and
 re-evaluates the schedule's element order with the fold kernel (ring: chunk c folded
@@ -33,14 +36,18 @@ XGMI_LINKS = 7
 
 
 # Measured transports: (name, shmemx_set_transport id, p2p signalling mode, RCCL native
-# allgather).  rccl runs twice: every round as grouped ncclSend/ncclRecv (the default) and
-# with the equal-chunk allgather round as one ncclAllGather (sosx_set_rccl_allgather);
-# p2p runs twice: counters moved between rounds by stream-ordered device signals (the
-# default) and by the host every round (sosx_set_p2p_signal_mode(0)).  Every leg
-# reports each.
-TRANSPORTS = (("rccl", 0, None, 0), ("rccl_ag", 0, None, 1), ("p2p", 1, 1, 0),
-              ("p2p_host", 1, 0, 0))
+# allgather, RCCL native allreduce mode).  rccl runs three ways: every round as grouped
+# ncclSend/ncclRecv (the default), with the equal-chunk allgather round as one
+# ncclAllGather (sosx_set_rccl_allgather), and as RCCL's own ncclAllReduce
+# (sosx_set_rccl_allreduce(2)); p2p runs twice: counters moved between rounds by
+# stream-ordered device signals (the default) and by the host every round
+# (sosx_set_p2p_signal_mode(0)).
+TRANSPORTS = (("rccl", 0, None, 0, 0), ("rccl_ag", 0, None, 1, 0), ("p2p", 1, 1, 0, 0),
+              ("p2p_host", 1, 0, 0, 0), ("rccl_ar", 0, None, 0, 2))
 T_NAMES = tuple(t[0] for t in TRANSPORTS)
+# the SOS schedules (bit-exact); rccl_ar ignores the schedule, so the schedule, host and
+# scan/broadcast legs skip it (the headline and the size curve measure it)
+SCHEDULE_T = ("rccl", "rccl_ag", "p2p", "p2p_host")
 
 # transports that failed the preflight on some rank (every leg skips them)
 DISABLED = set()
@@ -52,17 +59,24 @@ def use_transport(S, L, tname):
     """Switch every PE (collectively) to `tname`; False when it is unavailable."""
     if tname in DISABLED:
         return False
-    _, tid, sig, ag = next(t for t in TRANSPORTS if t[0] == tname)
+    _, tid, sig, ag, ar = next(t for t in TRANSPORTS if t[0] == tname)
     if S.lib().shmemx_set_transport(tid) < 0:
         return False
     L.lib().sosx_set_rccl_allgather(ag)
+    L.lib().sosx_set_rccl_allreduce(ar)
     return sig is None or L.lib().sosx_set_p2p_signal_mode(sig) >= 0
 
 
 def reset_transport(S, L):
     S.lib().shmemx_set_transport(0)
     L.lib().sosx_set_rccl_allgather(0)
+    L.lib().sosx_set_rccl_allreduce(0)
     L.lib().sosx_set_p2p_signal_mode(1)
+
+
+def tolerance_leg(tname, args):
+    """rccl_ar on fp sum/prod: RCCL's own summation order, checked against the fp bound."""
+    return tname == "rccl_ar" and args.dtype in ("float", "double") and args.op in ("sum", "prod")
 
 
 def log(*a):
@@ -101,7 +115,7 @@ def main(args, torch):
     if user_transport is None:
         # a transport that failed everywhere is not even brought up in this job
         p2p_any = pre["ok"]["p2p"] or pre["ok"]["p2p_host"]
-        rccl_any = pre["ok"]["rccl"] or pre["ok"]["rccl_ag"]
+        rccl_any = pre["ok"]["rccl"] or pre["ok"]["rccl_ag"] or pre["ok"]["rccl_ar"]
         if p2p_any != rccl_any:
             os.environ["SHMEMX_TRANSPORT"] = "p2p" if p2p_any else "rccl"
     if rank == 0 and DISABLED:
@@ -163,13 +177,17 @@ def main(args, torch):
         torch.cuda.synchronize()
         dist.barrier()
         step()
+        tol = tolerance_leg(tname, args)
         mm = self_check(torch, L, S, dt, L.op_id(args.op), dist_kind, check_seed, world, n, es,
-                        alg, dst, stream)
+                        alg, dst, stream, tolerance=tol)
+        mm, tv = mm if tol else (mm, 0)
         L.fill(dt, dist_kind, seed, rank, src, n, 0, stream)
         torch.cuda.synchronize()
-        mmt = torch.tensor([mm], dtype=torch.int64)
+        mmt = torch.tensor([mm, tv], dtype=torch.int64)
         dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
-        results[tname] = {"t_step": t_step, "prof": prof, "mismatches": int(mmt.item())}
+        results[tname] = {"t_step": t_step, "prof": prof, "mismatches": int(mmt[0].item())}
+        if tol:
+            results[tname]["tolerance_violations"] = int(mmt[1].item())
 
     curve = size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
                        src, dst, stream, sorted(sweep_sizes + [n]), results) if sweep_sizes else {}
@@ -214,7 +232,10 @@ def main(args, torch):
                 "frac_7_links": round(wire / ts / 1e9 / (XGMI_LINK_GBS * XGMI_LINKS), 3),
                 "xfer_ms_per_step": round(rr["prof"]["xfer_ms"] / max(rr["prof"]["ncall"], 1), 4),
                 "fold_ms_per_step": round(rr["prof"]["fold_ms"] / max(rr["prof"]["ncall"], 1), 4),
-                "bitwise_mismatches_all_ranks": rr["mismatches"]}
+                "bitwise_mismatches_all_ranks": rr["mismatches"],
+                **({"fp_tolerance_violations_all_ranks": rr["tolerance_violations"],
+                    "note": "RCCL's own order: compared with the fp bound, not bit for bit"}
+                   if "tolerance_violations" in rr else {})}
 
     res = {
         "metric": "GiB/s device-resident sum_reduce combine, nreduce=128Mi fp32; 1/2/4/8 GPU",
@@ -251,7 +272,9 @@ def main(args, torch):
                                "bitwise check; the library default is rccl "
                                "(SHMEMX_TRANSPORT selects; rccl_ag = rccl with "
                                "SHMEMX_RCCL_ALLGATHER=1, p2p_host = p2p with "
-                               "SHMEMX_P2P_SIGNAL=host)")
+                               "SHMEMX_P2P_SIGNAL=host, rccl_ar = RCCL's own ncclAllReduce "
+                               "with SHMEMX_RCCL_ALLREDUCE=2, the reference point: not SOS's "
+                               "order for fp sum, so not eligible for value then)")
     res["preflight"] = pre
     if curve:
         res["size_curve"] = curve
@@ -404,7 +427,7 @@ def host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, see
     host = np.ctypeslib.as_array((ctypes_u8 * nbytes).from_address(hsrc))
     host[:] = tmp.cpu().numpy()
     out = {"nreduce": m, "buffers": "shmem_malloc (pinned host symmetric heap)"}
-    for tid, tname in enumerate(T_NAMES):
+    for tid, tname in enumerate(SCHEDULE_T):
         if not headline.get(tname, {}).get("available", True) or not use_transport(S, L, tname):
             continue
         reps = max(3, min(args.steps, 10))
@@ -470,11 +493,15 @@ def size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank,
                 torch.cuda.synchronize()
                 dist.barrier()
                 fn(team, dst, src, m)
+                tol = tolerance_leg(tname, args)
                 mm = self_check(torch, L, S, dt, L.op_id(args.op), dist_kind, cseed, world, m, es,
-                                alg, dst, stream)
-                mmt = torch.tensor([mm], dtype=torch.int64)
+                                alg, dst, stream, tolerance=tol)
+                mm, tv = mm if tol else (mm, 0)
+                mmt = torch.tensor([mm, tv], dtype=torch.int64)
                 dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
-                row["bitwise_mismatches_all_ranks"] = int(mmt.item())
+                row["bitwise_mismatches_all_ranks"] = int(mmt[0].item())
+                if tol:
+                    row["fp_tolerance_violations_all_ranks"] = int(mmt[1].item())
                 L.fill(dt, dist_kind, seed, rank, src, args.n, 0, stream)
                 torch.cuda.synchronize()
             rows.append(row)
@@ -494,7 +521,7 @@ def other_schedules(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, 
     n, P = args.n, world
     out = {}
     steps = max(3, min(args.steps, 10))
-    for tid, tname in enumerate(T_NAMES):
+    for tid, tname in enumerate(SCHEDULE_T):
         if not headline.get(tname, {}).get("available", True) or not use_transport(S, L, tname):
             continue
         for sname in ("rechalving", "recdbl_direct"):
@@ -555,7 +582,7 @@ def adjacent_collectives(args, torch, dist, L, S, dt, es, n, src, dst, stream, s
     # broadcast: the root puts the payload on its links once (scattered over P-1 links
     # above 64 KiB); each non-root forwards its 1/(P-1) share to the P-2 others
     colls.append(("broadcast_root0", lambda: bcast_fn(team, dst, src, n, 0), n * es))
-    for tid, tname in enumerate(T_NAMES):
+    for tid, tname in enumerate(SCHEDULE_T):
         if not use_transport(S, L, tname):
             continue
         for cname, call, wire in colls:
@@ -610,8 +637,12 @@ def adjacent_collectives(args, torch, dist, L, S, dt, es, n, src, dst, stream, s
     return out
 
 
-def self_check(torch, L, S, dt, opid, dist_kind, seed, world, n, es, alg, dst, stream):
-    """Bitwise check of this rank's result against a local re-evaluation."""
+def self_check(torch, L, S, dt, opid, dist_kind, seed, world, n, es, alg, dst, stream,
+               tolerance=False):
+    """Bitwise check of this rank's result against a local re-evaluation.  With
+    `tolerance` (fp sum/prod, for results in another order than the schedule's) it
+    returns (bitwise mismatches, elements outside the fp bound of DESIGN.md section 5:
+    |got - exp| <= (P-1) eps sum_p |x_p| for sum, 2 (P-1) eps |exp| for prod)."""
     resolved = S.lib().sosx_resolve_alg(alg, n * es, 16384)
     ins = []
     for p in range(world):
@@ -632,8 +663,26 @@ def self_check(torch, L, S, dt, opid, dist_kind, seed, world, n, es, alg, dst, s
         L.fold(opid, dt, L.ORDER_TREE, exp.data_ptr(), [b.data_ptr() for b in ins], n, stream)
     torch.cuda.synchronize()
     bad = L.count_mismatch(exp.data_ptr(), dst, n, es, stream)
+    if not tolerance:
+        del ins
+        return bad
+    ft = {4: torch.float32, 8: torch.float64}[es]
+    got = torch.empty(n * es, dtype=torch.uint8, device="cuda")
+    L.check(L.lib().sosx_memcpy(got.data_ptr(), dst, n * es, stream), "sosx_memcpy")
+    torch.cuda.synchronize()
+    eps = torch.finfo(ft).eps
+    g = got.view(ft).double()
+    e = exp.view(ft).double()
+    if opid == L.op_id("sum"):
+        bound = torch.zeros_like(e)
+        for b in ins:
+            bound += b.view(ft).double().abs()
+        bound *= (world - 1) * eps
+    else:
+        bound = 2 * (world - 1) * eps * e.abs()
+    tol_bad = int(((g - e).abs() > bound).sum().item())
     del ins
-    return bad
+    return bad, tol_bad
 
 
 def preflight(torch, dist, rank, world):
@@ -739,8 +788,12 @@ def preflight_child():
             L.fill(dt, L.DIST_UNIFORM, seed, rank, src, n, 0, stream)
             torch.cuda.synchronize()
             S.shmem_float_sum_reduce(team, dst, src, n)
-            bad += self_check(torch, L, S, dt, L.op_id("sum"), L.DIST_UNIFORM, seed, world, n,
-                              es, alg, dst, stream)
+            if tname == "rccl_ar":   # RCCL's order: the fp bound, not the bits
+                bad += self_check(torch, L, S, dt, L.op_id("sum"), L.DIST_UNIFORM, seed, world,
+                                  n, es, alg, dst, stream, tolerance=True)[1]
+            else:
+                bad += self_check(torch, L, S, dt, L.op_id("sum"), L.DIST_UNIFORM, seed, world,
+                                  n, es, alg, dst, stream)
         print(json.dumps({"t": tname, "ok": bad == 0, "mismatches": bad}), flush=True)
     reset_transport(S, L)
     S.shmemx_free_device(dst)

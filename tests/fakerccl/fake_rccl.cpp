@@ -1,8 +1,8 @@
 // TEST INFRASTRUCTURE ONLY -- never linked into sos_amd/libsos_amd.so.
 //
-// A stand-in for the nine RCCL entry points libsos_amd.so calls (ncclGetUniqueId,
+// A stand-in for the ten RCCL entry points libsos_amd.so calls (ncclGetUniqueId,
 // ncclCommInitRank, ncclCommDestroy, ncclGetErrorString, ncclGroupStart/End, ncclSend,
-// ncclRecv, ncclAllGather), linked with hidden visibility into a test copy of the library,
+// ncclRecv, ncclAllGather, ncclAllReduce), linked with hidden visibility into a test copy of the library,
 // tests/fakerccl/libsos_amd_fakerccl.so.  Real RCCL refuses two ranks on one GPU
 // ("Duplicate GPU detected"), and the GPU box has one, so without this the RCCL executor
 // (collectives.cpp exec_rccl, the RCCL device barrier and team words in runtime.cpp) only
@@ -19,6 +19,9 @@
 //     and unlinks it.  It returns with all transfers complete.
 //   * ncclAllGather is a group of one send of the contribution to every peer and one
 //     receive from every peer into its slot, plus the local copy when not in place;
+//   * ncclAllReduce sends the whole send buffer to every peer, receives every peer's,
+//     and folds the P buffers on the host in rank order (sum/prod/min/max of the 8/32/64-bit
+//     integer and fp32/fp64 types; integers in two's complement);
 //   * messages of one ordered pair match in issue order through per-pair sequence numbers,
 //     RCCL's FIFO rule; a size mismatch or a wait longer than FAKERCCL_TIMEOUT seconds
 //     (default 120) returns an error, which libsos_amd.so turns into an abort.
@@ -56,7 +59,7 @@ struct Op {
 
 int g_depth = 0;
 std::vector<Op> g_ops;
-unsigned long long g_msgs = 0, g_bytes = 0, g_allgathers = 0;
+unsigned long long g_msgs = 0, g_bytes = 0, g_allgathers = 0, g_allreduces = 0;
 int g_rank = -1;
 
 // FAKERCCL_STATS=1: each process reports how much went through the stand-in, so a test can
@@ -65,8 +68,8 @@ __attribute__((destructor)) void report()
 {
     const char *e = getenv("FAKERCCL_STATS");
     if (e && *e == '1' && g_rank >= 0)
-        fprintf(stderr, "fakerccl stats: rank %d sent %llu messages, %llu bytes, %llu allgathers\n",
-                g_rank, g_msgs, g_bytes, g_allgathers);
+        fprintf(stderr, "fakerccl stats: rank %d sent %llu messages, %llu bytes, %llu allgathers, "
+                "%llu allreduces\n", g_rank, g_msgs, g_bytes, g_allgathers, g_allreduces);
 }
 
 double now_s()
@@ -291,6 +294,75 @@ ncclResult_t ncclAllGather(const void *sendbuff, void *recvbuff, size_t sendcoun
     if (r != ncclSuccess) return r;
     if (mine != sendbuff && bytes &&
         hipMemcpyAsync(mine, sendbuff, bytes, hipMemcpyDefault, stream) != hipSuccess)
+        return ncclUnhandledCudaError;
+    return ncclSuccess;
+}
+
+namespace {
+
+template <class T> void fold_into(T *acc, const T *x, size_t n, ncclRedOp_t op)
+{
+    for (size_t i = 0; i < n; ++i) {
+        switch (op) {
+        case ncclSum: acc[i] = (T)(acc[i] + x[i]); break;
+        case ncclProd: acc[i] = (T)(acc[i] * x[i]); break;
+        case ncclMin: acc[i] = x[i] < acc[i] ? x[i] : acc[i]; break;
+        case ncclMax: acc[i] = x[i] > acc[i] ? x[i] : acc[i]; break;
+        default: break;
+        }
+    }
+}
+
+// integer sum/prod in the unsigned type of the same width (two's-complement wrap, no UB)
+bool fold_typed(char *acc, const char *x, size_t n, ncclDataType_t t, ncclRedOp_t op)
+{
+    const bool arith = op == ncclSum || op == ncclProd;
+    switch (t) {
+    case ncclInt8: arith ? fold_into((uint8_t *)acc, (const uint8_t *)x, n, op)
+                         : fold_into((int8_t *)acc, (const int8_t *)x, n, op); return true;
+    case ncclUint8: fold_into((uint8_t *)acc, (const uint8_t *)x, n, op); return true;
+    case ncclInt32: arith ? fold_into((uint32_t *)acc, (const uint32_t *)x, n, op)
+                          : fold_into((int32_t *)acc, (const int32_t *)x, n, op); return true;
+    case ncclUint32: fold_into((uint32_t *)acc, (const uint32_t *)x, n, op); return true;
+    case ncclInt64: arith ? fold_into((uint64_t *)acc, (const uint64_t *)x, n, op)
+                          : fold_into((int64_t *)acc, (const int64_t *)x, n, op); return true;
+    case ncclUint64: fold_into((uint64_t *)acc, (const uint64_t *)x, n, op); return true;
+    case ncclFloat32: fold_into((float *)acc, (const float *)x, n, op); return true;
+    case ncclFloat64: fold_into((double *)acc, (const double *)x, n, op); return true;
+    default: return false;
+    }
+}
+
+}  // namespace
+
+ncclResult_t ncclAllReduce(const void *sendbuff, void *recvbuff, size_t count, ncclDataType_t t,
+                           ncclRedOp_t op, ncclComm_t comm, hipStream_t stream)
+{
+    const size_t ts = type_size(t);
+    if (!comm || !ts || g_depth || op < ncclSum || op > ncclMin) return ncclInvalidArgument;
+    const size_t bytes = count * ts;
+    const int P = comm->nranks;
+    ++g_allreduces;
+    if (hipStreamSynchronize(stream) != hipSuccess) return ncclUnhandledCudaError;
+    std::vector<std::vector<char>> all((size_t)P, std::vector<char>(bytes));
+    if (bytes && hipMemcpy(all[(size_t)comm->rank].data(), sendbuff, bytes, hipMemcpyDefault) != hipSuccess)
+        return ncclUnhandledCudaError;
+    std::vector<char> tmp;
+    for (int q = 0; q < P; ++q) {
+        if (q == comm->rank) continue;
+        const ncclResult_t r = post_send({true, const_cast<void *>(sendbuff), bytes, q, comm, stream}, tmp);
+        if (r != ncclSuccess) return r;
+    }
+    for (int q = 0; q < P; ++q) {
+        if (q == comm->rank) continue;
+        // receive into host memory: complete_recv copies with hipMemcpyDefault
+        const ncclResult_t r = complete_recv({false, all[(size_t)q].data(), bytes, q, comm, stream}, tmp);
+        if (r != ncclSuccess) return r;
+    }
+    std::vector<char> acc = all[0];
+    for (int q = 1; q < P; ++q)
+        if (!fold_typed(acc.data(), all[(size_t)q].data(), count, t, op)) return ncclInvalidArgument;
+    if (bytes && hipMemcpy(recvbuff, acc.data(), bytes, hipMemcpyDefault) != hipSuccess)
         return ncclUnhandledCudaError;
     return ncclSuccess;
 }

@@ -2,7 +2,7 @@
 
 Real RCCL refuses two ranks on one GPU, so these runs load a test build of the library,
 tests/fakerccl/libsos_amd_fakerccl.so: the same objects as sos_amd/libsos_amd.so, with the
-nine RCCL entry points it calls bound to tests/fakerccl/fake_rccl.cpp, which moves each
+ten RCCL entry points it calls bound to tests/fakerccl/fake_rccl.cpp, which moves each
 ncclSend/ncclRecv through a /dev/shm file with RCCL's per-pair FIFO matching.  Everything
 above those calls is the product code the 8-GPU node runs with SHMEMX_TRANSPORT=rccl: the
 plans, exec_rccl's byte offsets and groups, the folds between rounds, the striped
@@ -103,6 +103,30 @@ def test_api_sweep_rccl(np_=2):
     _ok(r, np_)
 
 
+@pytest.mark.parametrize("np_", [2, 3])
+def test_api_sweep_rccl_native_allreduce(np_):
+    """SHMEMX_RCCL_ALLREDUCE=1: every integer sum/prod/min/max of an 8/32/64-bit type over
+    the world team runs as one ncclAllReduce (counted by the stand-in, which folds in rank
+    order), and all 198 typed reductions still match the oracle's SOS schedules bit for
+    bit (integer results do not depend on the order); 16-bit, bitwise, fp, complex and
+    long double calls keep their schedules."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "api_sweep_pe.py")], timeout=600,
+               SHMEMX_RCCL_ALLREDUCE="1")
+    _ok(r, np_)
+    ar = {int(rk): int(a) for rk, a in
+          re.findall(r"fakerccl stats: rank (\d+) .* (\d+) allreduces", r.stderr)}
+    assert sorted(ar) == list(range(np_)) and min(ar.values()) > 0, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("np_", [2, 4])
+def test_team_check_rccl_native_allreduce(np_):
+    """The same switch under tools/team_check.py: world-team integer calls through
+    ncclAllReduce, split-team calls (not world-shaped) on their schedules, all bit-exact."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+               SHMEMX_RCCL_ALLREDUCE="1")
+    _ok(r, np_)
+
+
 def test_bench_team_leg_rccl():
     """bench.py's N > 1 line as the driver runs it on the 8-GPU node, transport forced to
     RCCL: the headline ring, the size curve, rechalving / recdbl_direct, and the
@@ -120,7 +144,13 @@ def test_bench_team_leg_rccl():
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert res["config"]["transport"] in ("rccl", "rccl_ag"), res["config"]
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0, res["check"]
-    assert list(res["transports"]) == ["rccl", "rccl_ag"], res["transports"]
+    assert list(res["transports"]) == ["rccl", "rccl_ag", "rccl_ar"], res["transports"]
+    # RCCL's own allreduce (the stand-in folds in rank order): within the fp bound; at
+    # P = 2 the two orders are a commutative swap, so also bit for bit
+    ar = res["transports"]["rccl_ar"]
+    assert ar["fp_tolerance_violations_all_ranks"] == 0 and ar["bitwise_mismatches_all_ranks"] == 0, ar
+    assert res["size_curve"]["rccl_ar"][-1]["fp_tolerance_violations_all_ranks"] == 0
+    assert "rccl_ar" not in res["schedules"] and "rccl_ar" not in res["host_resident"]
     for t in ("rccl", "rccl_ag"):
         assert res["transports"][t]["bitwise_mismatches_all_ranks"] == 0, res["transports"]
         for coll in res["adjacent_collectives"][t].values():
@@ -151,7 +181,7 @@ def test_bench_preflight_drops_a_hanging_transport():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert res["preflight"]["ok"] == {"rccl": True, "rccl_ag": True, "p2p": False,
-                                      "p2p_host": False}, res["preflight"]
+                                      "p2p_host": False, "rccl_ar": False}, res["preflight"]
     assert "timed out" in r.stderr, r.stderr[-3000:]
     assert list(res["transports"]) == ["rccl", "rccl_ag"], res["transports"]
     assert res["config"]["transport"] in ("rccl", "rccl_ag")

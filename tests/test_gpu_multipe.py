@@ -239,5 +239,6 @@ def test_bench_team_leg_default_transport():
     # the preflight job found RCCL down (init refused, every PE fell back) and p2p clean,
     # so this job brought up p2p only
     assert res["preflight"]["ran"] and res["preflight"]["ok"] == \
-        {"rccl": False, "rccl_ag": False, "p2p": True, "p2p_host": True}, res["preflight"]
-    assert "preflight: transports ['rccl', 'rccl_ag'] disabled" in r.stderr
+        {"rccl": False, "rccl_ag": False, "p2p": True, "p2p_host": True,
+         "rccl_ar": False}, res["preflight"]
+    assert "preflight: transports ['rccl', 'rccl_ag', 'rccl_ar'] disabled" in r.stderr

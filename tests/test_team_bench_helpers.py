@@ -17,6 +17,10 @@ class _Lib:
         self.calls.append(("allgather", on))
         return 0
 
+    def sosx_set_rccl_allreduce(self, mode):
+        self.calls.append(("allreduce", mode))
+        return 0
+
     def sosx_set_p2p_signal_mode(self, mode):
         self.calls.append(("signal", mode))
         return -1 if (mode == 1 and not self.stream_ok) else 0
@@ -33,21 +37,22 @@ class _Wrap:
 def test_use_transport_selects_transport_and_signal_mode():
     lib = _Lib({0, 1}, stream_ok=True)
     S = L = _Wrap(lib)
-    assert TB.T_NAMES == ("rccl", "rccl_ag", "p2p", "p2p_host")
-    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [True, True, True, True]
-    assert lib.calls == [("transport", 0), ("allgather", 0),
-                         ("transport", 0), ("allgather", 1),
-                         ("transport", 1), ("allgather", 0), ("signal", 1),
-                         ("transport", 1), ("allgather", 0), ("signal", 0)]
+    assert TB.T_NAMES == ("rccl", "rccl_ag", "p2p", "p2p_host", "rccl_ar")
+    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [True] * 5
+    assert lib.calls == [("transport", 0), ("allgather", 0), ("allreduce", 0),
+                         ("transport", 0), ("allgather", 1), ("allreduce", 0),
+                         ("transport", 1), ("allgather", 0), ("allreduce", 0), ("signal", 1),
+                         ("transport", 1), ("allgather", 0), ("allreduce", 0), ("signal", 0),
+                         ("transport", 0), ("allgather", 0), ("allreduce", 2)]
     lib.calls.clear()
     TB.reset_transport(S, L)
-    assert lib.calls == [("transport", 0), ("allgather", 0), ("signal", 1)]
+    assert lib.calls == [("transport", 0), ("allgather", 0), ("allreduce", 0), ("signal", 1)]
 
 
 def test_unavailable_transports_report_false():
     lib = _Lib({1}, stream_ok=False)   # RCCL down, stream signalling unavailable
     S = L = _Wrap(lib)
-    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [False, False, False, True]
+    assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [False, False, False, True, False]
 
 
 class _Dist:
@@ -104,7 +109,8 @@ def test_preflight_child_died_mid_way(monkeypatch):
     died in and every one it never reached count as failed."""
     out = 'noise\n{"t": "rccl", "ok": true}\n{"t": "rccl_ag", "ok": true}\n'
     pre = _run_preflight(monkeypatch, out, rc=1)
-    assert pre["ok"] == {"rccl": True, "rccl_ag": True, "p2p": False, "p2p_host": False}
+    assert pre["ok"] == {"rccl": True, "rccl_ag": True, "p2p": False, "p2p_host": False,
+                         "rccl_ar": False}
     assert pre["why"] == "child rc=1"
 
 
@@ -112,7 +118,8 @@ def test_preflight_mismatch_and_timeout(monkeypatch):
     out = ('{"t": "rccl", "ok": true}\n{"t": "rccl_ag", "ok": false, "mismatches": 3}\n'
            '{"t": "p2p", "ok": true}\n')
     pre = _run_preflight(monkeypatch, out, timeout=True)
-    assert pre["ok"] == {"rccl": True, "rccl_ag": False, "p2p": True, "p2p_host": False}
+    assert pre["ok"] == {"rccl": True, "rccl_ag": False, "p2p": True, "p2p_host": False,
+                         "rccl_ar": False}
     assert pre["why"] == "child killed after 0 s"
 
 
@@ -121,7 +128,7 @@ def test_preflight_disabled_transports_are_skipped():
     S = L = _Wrap(lib)
     TB.DISABLED.update({"p2p", "rccl_ag"})
     try:
-        assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [True, False, False, True]
+        assert [TB.use_transport(S, L, t) for t in TB.T_NAMES] == [True, False, False, True, True]
     finally:
         TB.DISABLED.clear()
 
