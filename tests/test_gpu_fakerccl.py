@@ -162,6 +162,32 @@ def test_bench_team_leg_rccl():
         assert curve[-1]["bitwise_mismatches_all_ranks"] == 0   # 4Mi: equal chunks
 
 
+def test_bench_rccl_allreduce_is_checked_by_tolerance():
+    """Four PEs: RCCL's own allreduce order (the stand-in folds in rank order) differs
+    from SOS's ring for fp sum, so rccl_ar shows bitwise mismatches, stays inside the fp
+    bound, and is never the transport `value` comes from.  (Not 3: the bench's inputs
+    are multiples of 2^-23 in [-1, 1), so every partial sum of two is exact and 3-PE sums
+    agree in any order.)"""
+    env = _env()
+    port = 29050 + os.getpid() % 500
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=4", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "4", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-host",
+                        "--no-adjacent", "--nreduce", str((1 << 20) + 3),
+                        "--sweep-max", str(4 << 20)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    ar = res["transports"]["rccl_ar"]
+    assert ar["bitwise_mismatches_all_ranks"] > 0, ar
+    assert ar["fp_tolerance_violations_all_ranks"] == 0, ar
+    assert res["size_curve"]["rccl_ar"][-1]["fp_tolerance_violations_all_ranks"] == 0
+    assert res["config"]["transport"] in ("rccl", "rccl_ag"), res["config"]
+    assert res["check"]["bitwise_mismatches_all_ranks"] == 0
+    assert res["preflight"]["ok"]["rccl_ar"], res["preflight"]
+
+
 def test_bench_preflight_drops_a_hanging_transport():
     """The N > 1 bench's preflight against a transport that hangs: both transports are up
     (SHMEMX_TRANSPORT=both, RCCL through the stand-in), and in the preflight job PE 1
