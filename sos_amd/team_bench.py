@@ -262,7 +262,10 @@ def main(args, torch):
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(fold_bytes / (fold_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if fold_ms > 0 else None,
                      "traffic": None, "algorithmic_bytes_per_launch": fold_bytes,
-                     "mean_kernel_ms": round(fold_ms, 5)},
+                     "mean_kernel_ms": round(fold_ms, 5),
+                     **({"note": "p2p: the fold reads its P-1 peer inputs in place over xGMI, "
+                                 "so this launch is link-bound (see team_roofline)"}
+                        if primary.startswith("p2p") else {})},
         "team_roofline": dict(bound="xgmi", wire_bytes_per_pe=int(wire), **team_roof(r)),
         "check": {"bitwise_mismatches_all_ranks": r["mismatches"],
                   "against": "on-GPU regeneration of all PE inputs + schedule-order fold"},
