@@ -209,6 +209,8 @@ def main(args, torch):
         adjacent = adjacent_collectives(args, torch, dist, L, S, dt, es, n, src, dst, stream,
                                         seed, rank, world)
 
+    local_leg = local_combine(args, torch, dist, L, dt, es, n, src, dst, stream, world)
+
     # `value` is the faster transport among those whose bitwise check is clean (both are
     # the library's: SHMEMX_TRANSPORT=rccl|p2p); every measured transport is reported
     measured = [k for k in T_NAMES if results[k].get("available", True)]
@@ -279,6 +281,7 @@ def main(args, torch):
                                "with SHMEMX_RCCL_ALLREDUCE=2, the reference point: not SOS's "
                                "order for fp sum, so not eligible for value then)")
     res["preflight"] = pre
+    res["local_combine_all_pes"] = local_leg
     if curve:
         res["size_curve"] = curve
     if schedules:
@@ -297,6 +300,33 @@ def main(args, torch):
     S.shmem_finalize()
     dist.destroy_process_group()
     return 0
+
+
+def local_combine(args, torch, dist, L, dt, es, n, src, dst, stream, world):
+    """The N = 1 headline kernel on every GPU at once (reduce_local: dst OP= src, nreduce
+    per PE, no exchange): the local HBM roofline at N GPUs, beside the team line's xGMI
+    one.  Whole-job GiB/s = world * n * s / max-over-ranks time per call."""
+    opid = L.op_id(args.op)
+    steps = max(5, min(args.steps, 50))
+    for _ in range(3):
+        L.combine(opid, dt, dst, src, n, stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        L.combine(opid, dt, dst, src, n, stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    el = torch.tensor([t1 - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    ts = el.item() / steps
+    return {"kernel": "sos::k_combine3", "nreduce": n, "ms_per_call": round(ts * 1e3, 4),
+            "value_GiBs": round(world * n * es / ts / GiB, 3),
+            "hbm_GBs_per_pe": round(3 * n * es / ts / 1e9, 1),
+            "frac_of_hbm_peak_per_pe": round(3 * n * es / ts / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "every PE's local combine at once, no exchange (host wall clock, "
+                    "max over ranks): the HBM side of the 1->N curve; per PE = per GPU "
+                    "with one PE per GPU"}
 
 
 def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,

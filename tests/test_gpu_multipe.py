@@ -143,6 +143,8 @@ def test_bench_team_leg(np_):
         curve = res["size_curve"][t]
         assert [r["nreduce"] for r in curve] == [1 << 20, (1 << 20) + 3, 4 << 20]
         assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
+    # the local combine on every PE at once (the HBM side of the curve)
+    assert res["local_combine_all_pes"]["value_GiBs"] > 0, res["local_combine_all_pes"]
     # SOS's ring on np_ host processes beside the line, equal to the GPU ring byte for byte
     cpu = res["cpu_ring_baseline"]
     assert cpu["cores"] == np_ and cpu["value"] > 0 and cpu["kind"] == "port", cpu
