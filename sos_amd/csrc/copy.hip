@@ -8,6 +8,10 @@
 // body of each segment, bytes for the ragged ends.
 #include "elementwise.h"
 
+#ifndef GATHER_U
+#define GATHER_U 4
+#endif
+
 namespace sos {
 
 constexpr int kMaxSeg = 16;
@@ -63,7 +67,7 @@ struct GatherArgs {
     uint64_t head[kMaxSeg];    // bytes before the 16-B aligned body
     uint64_t nvec[kMaxSeg];    // 16-B vectors in the body
     uint64_t bytes[kMaxSeg];
-    uint64_t vstart[kMaxSeg + 1];  // prefix sums of nvec
+    uint64_t tstart[kMaxSeg + 1];  // prefix sums of each segment's tiles
     int nseg;
 };
 
@@ -76,27 +80,43 @@ struct GatherArgs {
 constexpr int kMaxGate = 16;
 constexpr unsigned kGateMaxBlocks = 16;
 
+// One tile of kGatherU 16-B vectors per lane, one tile per workgroup (the combine's
+// shape: every load of the tile issued before the first store, no grid-stride loop);
+// a tile lies in one segment, so the segment lookup is uniform per workgroup.
+constexpr int kGatherU = GATHER_U;
+constexpr uint64_t kTileVec = (uint64_t)kThreads * kGatherU;
+
 template <bool GATED>
 __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g, Sig<kMaxGate> gate)
 {
     if constexpr (GATED) sig_step(gate, threadIdx.x);
-    const uint64_t total = g.vstart[g.nseg];
-    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
-    int s = 0;
-    for (uint64_t v = (uint64_t)blockIdx.x * kThreads + threadIdx.x; v < total; v += stride) {
-        while (v >= g.vstart[s + 1]) ++s;
-        const uint64_t j = v - g.vstart[s];
+    const uint64_t t = blockIdx.x;
+    if (t < g.tstart[g.nseg]) {
+        int s = 0;
+        while (t >= g.tstart[s + 1]) ++s;
         const u32x4 *src = reinterpret_cast<const u32x4 *>(g.src[s] + g.head[s]);
         u32x4 *dst = reinterpret_cast<u32x4 *>(g.dst[s] + g.head[s]);
-        __builtin_nontemporal_store(__builtin_nontemporal_load(src + j), dst + j);
+        const uint64_t j0 = (t - g.tstart[s]) * kTileVec + threadIdx.x;
+        const uint64_t nv = g.nvec[s];
+        u32x4 v[kGatherU];
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * kThreads;
+            if (j < nv) v[u] = __builtin_nontemporal_load(src + j);
+        }
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+            const uint64_t j = j0 + (uint64_t)u * kThreads;
+            if (j < nv) __builtin_nontemporal_store(v[u], dst + j);
+        }
     }
     // ragged ends: the last workgroup copies them byte by byte
     if (blockIdx.x == gridDim.x - 1) {
-        for (int t = 0; t < g.nseg; ++t) {
-            for (uint64_t b = threadIdx.x; b < g.head[t]; b += kThreads) g.dst[t][b] = g.src[t][b];
-            const uint64_t tail0 = g.head[t] + g.nvec[t] * 16;
-            for (uint64_t b = tail0 + threadIdx.x; b < g.bytes[t]; b += kThreads)
-                g.dst[t][b] = g.src[t][b];
+        for (int t2 = 0; t2 < g.nseg; ++t2) {
+            for (uint64_t b = threadIdx.x; b < g.head[t2]; b += kThreads) g.dst[t2][b] = g.src[t2][b];
+            const uint64_t tail0 = g.head[t2] + g.nvec[t2] * 16;
+            for (uint64_t b = tail0 + threadIdx.x; b < g.bytes[t2]; b += kThreads)
+                g.dst[t2][b] = g.src[t2][b];
         }
     }
 }
@@ -128,7 +148,8 @@ int launch_step(const Sig<kMaxGate> &gate, hipStream_t st)
     return hip_ok(hipGetLastError());
 }
 
-// Copy nseg (src, dst, bytes) segments, <= 16 per launch.  `gate` (or null): a signalling
+// Copy nseg (src, dst, bytes) segments, <= 16 per launch.  (A gate rides in the launch
+// when it has at most kGateMaxBlocks tiles.)  `gate` (or null): a signalling
 // step that must precede the copies -- carried by the first launch when its grid is
 // small enough, else run by its own k_p2p_signal launch first.
 int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,
@@ -155,16 +176,15 @@ int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size
                 g.head[n] = bytes[i];  // incongruent: all bytes by the byte loop
                 g.nvec[n] = 0;
             }
-            g.vstart[n] = tot;
-            tot += g.nvec[n];
+            g.tstart[n] = tot;
+            tot += (g.nvec[n] + kTileVec - 1) / kTileVec;
             ++n;
         }
         if (!n) continue;
         g.nseg = n;
-        g.vstart[n] = tot;
-        uint64_t blocks = (tot + kThreads * 4 - 1) / (kThreads * 4);
-        if (blocks < 1) blocks = 1;
-        if (blocks > 16384) blocks = 16384;
+        g.tstart[n] = tot;
+        const uint64_t blocks = tot ? tot : 1;  // one tile per workgroup (+ the ragged ends)
+        if (blocks > 0xffffffffull) return SOSX_ERR_ARG;
         Sig<kMaxGate> none;
         memset(&none, 0, sizeof(none));
         if (gate_pending && blocks <= kGateMaxBlocks) {

@@ -178,3 +178,42 @@ def test_loopback_reduce_twelve_pes(torch_cuda, alg):
         ref = O.ring(op, dt, srcs) if alg == "ring" else O.recdbl(op, dt, srcs)
         for p in range(P):
             assert np.array_equal(bits(got[p]), bits(ref[p])), (alg, n, p)
+
+
+@pytest.mark.parametrize("case", ["allgather8", "ragged", "incongruent", "many", "tiny"])
+def test_gather_kernel(torch_cuda, case):
+    """sosx_gather (the p2p transport's multi-segment copy, copy.hip k_gather): one tile
+    per workgroup over the 16-B congruent bodies, byte loops for the ragged ends and for
+    segments whose source and destination are not 16-B congruent; more than 16 segments
+    split into several launches.  Every destination byte must equal its source byte, and
+    bytes around the segments stay untouched."""
+    import ctypes
+    torch = torch_cuda
+    rng = np.random.default_rng(7)
+    if case == "allgather8":
+        segs = [(0, 0, 4 << 20)] * 7
+    elif case == "ragged":
+        segs = [(3, 3, 1000003), (16, 16, 65536 + 5), (1, 1, 17), (8, 8, 4096 * 16 + 1)]
+    elif case == "incongruent":
+        segs = [(1, 2, 100000), (5, 0, 33), (0, 7, 70000)]
+    elif case == "many":
+        segs = [(int(rng.integers(0, 16)),) * 2 + (int(rng.integers(1, 200000)),) for _ in range(37)]
+    else:
+        segs = [(0, 0, 1), (15, 15, 15), (4, 9, 0)]
+    srcs, dsts, sp, dp, nb = [], [], [], [], []
+    for so, do, n in segs:
+        s = torch.from_numpy(rng.integers(0, 256, n + 64, dtype=np.uint8)).cuda()
+        d = torch.full((n + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+        srcs.append((s, so, n))
+        dsts.append((d, do, n))
+        sp.append(s.data_ptr() + so)
+        dp.append(d.data_ptr() + do)
+        nb.append(n)
+    k = len(segs)
+    rc = _lib.lib().sosx_gather(k, (ctypes.c_void_p * k)(*sp), (ctypes.c_void_p * k)(*dp),
+                                (ctypes.c_size_t * k)(*nb), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    for (s, so, n), (d, do, _) in zip(srcs, dsts):
+        assert torch.equal(d[do:do + n], s[so:so + n])
+        assert bool((d[:do] == 0xA5).all()) and bool((d[do + n:] == 0xA5).all())
