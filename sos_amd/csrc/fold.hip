@@ -213,22 +213,33 @@ struct PrefixPtrs {
     void *out[kMaxPrefix];
 };
 
-template <class T, class OP, int NP>
+#ifndef PREFIX_U
+#define PREFIX_U 1
+#endif
+constexpr int kPrefixU = PREFIX_U;  // 16-B vectors per lane per tile
+
+template <class T, class OP, int NP, int U>
 __global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
 {
     constexpr int V = Pack<T>::N;
     for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
-        const size_t i = t * (size_t)kThreads + threadIdx.x;
-        u32x4 x[NP];
+        const size_t base = t * (size_t)(kThreads * U) + threadIdx.x;
+        u32x4 x[U][NP];
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            x[k] = ldv<true>(reinterpret_cast<const u32x4 *>((const T *)p.in[k] + g.head) + i);
-        u32x4 acc = x[0];
-        stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[0] + g.head) + i, acc);
 #pragma unroll
-        for (int k = 1; k < NP; ++k) {
-            acc = apply<T, OP>(acc, x[k]);
-            stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[k] + g.head) + i, acc);
+            for (int u = 0; u < U; ++u)
+                x[u][k] = ldv<true>(reinterpret_cast<const u32x4 *>((const T *)p.in[k] + g.head) + base + u * kThreads);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + u * kThreads;
+            u32x4 acc = x[u][0];
+            stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[0] + g.head) + i, acc);
+#pragma unroll
+            for (int k = 1; k < NP; ++k) {
+                acc = apply<T, OP>(acc, x[u][k]);
+                stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[k] + g.head) + i, acc);
+            }
         }
     }
     if (g.has_rem && blockIdx.x == gridDim.x - 1) {
@@ -245,7 +256,7 @@ __global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
             }
         };
         for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
-        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n; i += kThreads)
             one(i);
     }
 }
@@ -364,8 +375,8 @@ template <class T, class OP, int NP>
 int launch_prefix_np(const PrefixPtrs &p, size_t n, hipStream_t st)
 {
     const uintptr_t o = (uintptr_t)p.out[0];
-    Geom g = make_geom(o, n, sizeof(T), 1);
-    hipLaunchKernelGGL((k_prefix<T, OP, NP>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st, p, g);
+    Geom g = make_geom(o, n, sizeof(T), kPrefixU);
+    hipLaunchKernelGGL((k_prefix<T, OP, NP, kPrefixU>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st, p, g);
     return hip_ok(hipGetLastError());
 }
 
