@@ -218,7 +218,8 @@ struct PrefixPtrs {
 #endif
 constexpr int kPrefixU = PREFIX_U;  // 16-B vectors per lane per tile
 
-template <class T, class OP, int NP, int U>
+// NT: nontemporal loads/stores (the default); the plain variant is a bench A/B only.
+template <class T, class OP, int NP, int U, bool NT = true>
 __global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
 {
     constexpr int V = Pack<T>::N;
@@ -229,16 +230,16 @@ __global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
         for (int k = 0; k < NP; ++k)
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                x[u][k] = ldv<true>(reinterpret_cast<const u32x4 *>((const T *)p.in[k] + g.head) + base + u * kThreads);
+                x[u][k] = ldv<NT>(reinterpret_cast<const u32x4 *>((const T *)p.in[k] + g.head) + base + u * kThreads);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t i = base + u * kThreads;
             u32x4 acc = x[u][0];
-            stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[0] + g.head) + i, acc);
+            stv<NT>(reinterpret_cast<u32x4 *>((T *)p.out[0] + g.head) + i, acc);
 #pragma unroll
             for (int k = 1; k < NP; ++k) {
                 acc = apply<T, OP>(acc, x[u][k]);
-                stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[k] + g.head) + i, acc);
+                stv<NT>(reinterpret_cast<u32x4 *>((T *)p.out[k] + g.head) + i, acc);
             }
         }
     }
@@ -289,6 +290,7 @@ using namespace sos;
 namespace {
 
 int g_fold_variant = 0;  // tuning experiments on the 8-input fp32 sum fold (bench A/B)
+int g_prefix_variant = 0;  // same for the 8-input fp32 sum prefix
 
 template <class T, class OP, int NP, int ORDER, int U>
 int launch_fold_u(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
@@ -371,10 +373,24 @@ struct FoldFn {
     }
 };
 
+template <class T, class OP, int NP, int U, bool NT>
+int launch_prefix_u(const PrefixPtrs &p, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), U);
+    hipLaunchKernelGGL((k_prefix<T, OP, NP, U, NT>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st, p, g);
+    return hip_ok(hipGetLastError());
+}
+
 template <class T, class OP, int NP>
 int launch_prefix_np(const PrefixPtrs &p, size_t n, hipStream_t st)
 {
     const uintptr_t o = (uintptr_t)p.out[0];
+    if constexpr (std::is_same<T, float>::value && std::is_same<OP, OpSum>::value && NP == 8) {
+        if (g_prefix_variant == 1) return launch_prefix_u<T, OP, NP, 2, true>(p, n, st);
+        if (g_prefix_variant == 2) return launch_prefix_u<T, OP, NP, 4, true>(p, n, st);
+        if (g_prefix_variant == 3) return launch_prefix_u<T, OP, NP, 1, false>(p, n, st);
+        if (g_prefix_variant == 4) return launch_prefix_u<T, OP, NP, 2, false>(p, n, st);
+    }
     Geom g = make_geom(o, n, sizeof(T), kPrefixU);
     hipLaunchKernelGGL((k_prefix<T, OP, NP, kPrefixU>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st, p, g);
     return hip_ok(hipGetLastError());
@@ -441,6 +457,15 @@ int sosx_set_fold_variant(int v)
 {
     const int prev = g_fold_variant;
     if (v >= 0 && v <= 7) g_fold_variant = v;
+    return prev;
+}
+
+// Same for the 8-input fp32 sum prefix: 0 = default (U=1, nontemporal), 1 = U=2,
+// 2 = U=4, 3 = U=1 plain loads/stores, 4 = U=2 plain.  Returns the previous value.
+int sosx_set_prefix_variant(int v)
+{
+    const int prev = g_prefix_variant;
+    if (v >= 0 && v <= 4) g_prefix_variant = v;
     return prev;
 }
 

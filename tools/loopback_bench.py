@@ -26,9 +26,14 @@ def main():
     ap.add_argument("--fold-ab", action="store_true",
                     help="interleaved A/B of the fold variants (sosx_set_fold_variant) on P "
                          "resident chunks of n/P elements")
+    ap.add_argument("--prefix-ab", action="store_true",
+                    help="interleaved A/B of the scan prefix variants (sosx_set_prefix_variant) "
+                         "on P resident chunks of n/P elements")
     a = ap.parse_args()
     if a.fold_ab:
         return fold_ab(a)
+    if a.prefix_ab:
+        return prefix_ab(a)
     import torch
     from sos_amd import _lib as L
     from sos_amd import shmem as S
@@ -112,6 +117,45 @@ def fold_ab(a, rounds=7, reps=20):
         ms = sorted(res[v])[len(res[v]) // 2]
         rows[name] = {"median_ms": round(ms, 5), "GBs": round(algo / (ms / 1e3) / 1e9, 1)}
     print(json.dumps({"fold_ab": rows, "P": a.P, "chunk": chunk, "bytes": algo,
+                      "variants_bit_identical": same}))
+
+
+def prefix_ab(a, rounds=7, reps=20):
+    import torch
+    from sos_amd import _lib as L
+    torch.cuda.set_device(0)
+    dt = L.dtype_id(a.dtype)
+    es = L.dtype_size(dt)
+    chunk = a.n // a.P
+    ins = [torch.empty(chunk * es, dtype=torch.uint8, device="cuda") for _ in range(a.P)]
+    for k, b in enumerate(ins):
+        L.fill(dt, 0, 0x5EED, k, b.data_ptr(), chunk)
+    names = ("u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain")
+    outs = {v: [torch.empty_like(ins[0]) for _ in range(a.P)] for v in range(len(names))}
+    lib = L.lib()
+    ip = [b.data_ptr() for b in ins]
+    res = {v: [] for v in range(len(names))}
+    for _ in range(rounds):
+        for v in range(len(names)):
+            lib.sosx_set_prefix_variant(v)
+            op_ = [b.data_ptr() for b in outs[v]]
+            for _ in range(3):
+                L.prefix(a.op, dt, op_, ip, chunk, -1)
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            for _ in range(reps):
+                L.prefix(a.op, dt, op_, ip, chunk, -1)
+            s1.record()
+            torch.cuda.synchronize()
+            res[v].append(s0.elapsed_time(s1) / reps)
+    lib.sosx_set_prefix_variant(0)
+    same = all(torch.equal(x, y) for v in range(1, len(names)) for x, y in zip(outs[0], outs[v]))
+    algo = 2 * a.P * chunk * es
+    rows = {}
+    for v, name in enumerate(names):
+        ms = sorted(res[v])[len(res[v]) // 2]
+        rows[name] = {"median_ms": round(ms, 5), "GBs": round(algo / (ms / 1e3) / 1e9, 1)}
+    print(json.dumps({"prefix_ab": rows, "P": a.P, "chunk": chunk, "bytes": algo,
                       "variants_bit_identical": same}))
 
 
