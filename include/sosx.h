@@ -198,8 +198,8 @@ int sosx_num_combine_variants(void);
 const char *sosx_combine_variant_name(int variant);
 /* Same for the 8-input fp32 sum fold: 0 = default (U=1), 1 = U=2, 2 = U=4. */
 int sosx_set_fold_variant(int variant);
-/* Same for the 8-input fp32 sum prefix (scans): 0 = default (U=1, nontemporal),
- * 1 = U=2, 2 = U=4, 3 = U=1 plain loads/stores, 4 = U=2 plain. */
+/* Same for the fp32 sum prefix (scans, 2..8 inputs): 0 = default, 1 = U=2, 2 = U=4,
+ * 3 = U=1 plain loads/stores, 4 = U=2 plain, 5 = U=8 (U = 16-B vectors per lane). */
 int sosx_set_prefix_variant(int variant);
 
 /* Library / build identification. */

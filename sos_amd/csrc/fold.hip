@@ -385,7 +385,8 @@ template <class T, class OP, int NP>
 int launch_prefix_np(const PrefixPtrs &p, size_t n, hipStream_t st)
 {
     const uintptr_t o = (uintptr_t)p.out[0];
-    if constexpr (std::is_same<T, float>::value && std::is_same<OP, OpSum>::value && NP == 8) {
+    if constexpr (std::is_same<T, float>::value && std::is_same<OP, OpSum>::value && NP >= 2) {
+        if (g_prefix_variant == 5) return launch_prefix_u<T, OP, NP, 8, true>(p, n, st);
         if (g_prefix_variant == 1) return launch_prefix_u<T, OP, NP, 2, true>(p, n, st);
         if (g_prefix_variant == 2) return launch_prefix_u<T, OP, NP, 4, true>(p, n, st);
         if (g_prefix_variant == 3) return launch_prefix_u<T, OP, NP, 1, false>(p, n, st);
@@ -461,11 +462,11 @@ int sosx_set_fold_variant(int v)
 }
 
 // Same for the 8-input fp32 sum prefix: 0 = default (U=1, nontemporal), 1 = U=2,
-// 2 = U=4, 3 = U=1 plain loads/stores, 4 = U=2 plain.  Returns the previous value.
+// 2 = U=4, 3 = U=1 plain loads/stores, 4 = U=2 plain, 5 = U=8.  Returns the previous value.
 int sosx_set_prefix_variant(int v)
 {
     const int prev = g_prefix_variant;
-    if (v >= 0 && v <= 4) g_prefix_variant = v;
+    if (v >= 0 && v <= 5) g_prefix_variant = v;
     return prev;
 }
 

@@ -120,25 +120,34 @@ def fold_ab(a, rounds=7, reps=20):
                       "variants_bit_identical": same}))
 
 
-def prefix_ab(a, rounds=7, reps=20):
+def prefix_ab(a, rounds=9, reps=20):
+    """Every round draws a fresh buffer layout (each of the 2P buffers starts a random
+    number of 4 KiB pages into its allocation), since the relative placement of 16
+    concurrent streams moves the rate by several percent; the variants are then timed
+    interleaved on that layout.  Reports the median and range over layouts."""
+    import random
     import torch
     from sos_amd import _lib as L
     torch.cuda.set_device(0)
     dt = L.dtype_id(a.dtype)
     es = L.dtype_size(dt)
     chunk = a.n // a.P
-    ins = [torch.empty(chunk * es, dtype=torch.uint8, device="cuda") for _ in range(a.P)]
-    for k, b in enumerate(ins):
-        L.fill(dt, 0, 0x5EED, k, b.data_ptr(), chunk)
-    names = ("u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain")
-    outs = {v: [torch.empty_like(ins[0]) for _ in range(a.P)] for v in range(len(names))}
+    names = ("u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain", "u8_nt")
     lib = L.lib()
-    ip = [b.data_ptr() for b in ins]
+    rng = random.Random(1234)
     res = {v: [] for v in range(len(names))}
+    same = True
+    pages = 64
     for _ in range(rounds):
+        bufs = [torch.empty(chunk * es + pages * 4096, dtype=torch.uint8, device="cuda")
+                for _ in range(2 * a.P)]
+        ptrs = [b.data_ptr() + rng.randrange(pages) * 4096 for b in bufs]
+        ip, op_ = ptrs[:a.P], ptrs[a.P:]
+        for k, x in enumerate(ip):
+            L.fill(dt, 0, 0x5EED, k, x, chunk)
+        ref = None
         for v in range(len(names)):
             lib.sosx_set_prefix_variant(v)
-            op_ = [b.data_ptr() for b in outs[v]]
             for _ in range(3):
                 L.prefix(a.op, dt, op_, ip, chunk, -1)
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -148,16 +157,23 @@ def prefix_ab(a, rounds=7, reps=20):
             s1.record()
             torch.cuda.synchronize()
             res[v].append(s0.elapsed_time(s1) / reps)
-    lib.sosx_set_prefix_variant(0)
-    same = all(torch.equal(x, y) for v in range(1, len(names)) for x, y in zip(outs[0], outs[v]))
+            last = bufs[-1].clone()  # the final output (holds every input's contribution)
+            if ref is None:
+                ref = last
+            else:
+                same &= torch.equal(ref, last)
+        lib.sosx_set_prefix_variant(0)
+        del bufs, ref, last
     algo = 2 * a.P * chunk * es
     rows = {}
     for v, name in enumerate(names):
-        ms = sorted(res[v])[len(res[v]) // 2]
-        rows[name] = {"median_ms": round(ms, 5), "GBs": round(algo / (ms / 1e3) / 1e9, 1)}
+        ms = sorted(res[v])
+        rows[name] = {"median_ms": round(ms[len(ms) // 2], 5),
+                      "GBs": round(algo / (ms[len(ms) // 2] / 1e3) / 1e9, 1),
+                      "GBs_range": [round(algo / (ms[-1] / 1e3) / 1e9, 1),
+                                    round(algo / (ms[0] / 1e3) / 1e9, 1)]}
     print(json.dumps({"prefix_ab": rows, "P": a.P, "chunk": chunk, "bytes": algo,
-                      "variants_bit_identical": same}))
-
+                      "layouts": rounds, "variants_bit_identical": same}))
 
 if __name__ == "__main__":
     main()
