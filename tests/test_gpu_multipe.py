@@ -206,8 +206,13 @@ def test_team_check_host_stripes(np_, signal):
     chunk slices the host-buffer calls of tools/team_check.py run as many stripes plus
     the n mod P remainder stripe (p2p stripes only when SHMEMX_HOST_STRIPE_BYTES is set),
     bit for bit against the schedule-order fold."""
+    env = {"SHMEMX_HOST_STRIPE_BYTES": "256", "SHMEMX_P2P_SIGNAL": signal}
+    if np_ >= 8:
+        # eight processes' default hardware queues oversubscribe one GPU (DESIGN §7,
+        # profiles/r2_onegpu_hw_queue_oversubscription.txt): 72 s with 4 queues each
+        env["GPU_MAX_HW_QUEUES"] = "1"
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
-               extra_env={"SHMEMX_HOST_STRIPE_BYTES": "256", "SHMEMX_P2P_SIGNAL": signal})
+               extra_env=env)
     ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)\)", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
         r.stdout + r.stderr[-3000:]
