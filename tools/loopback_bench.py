@@ -82,42 +82,59 @@ def main():
     print(json.dumps(out))
 
 
-def fold_ab(a, rounds=7, reps=20):
+def fold_ab(a, rounds=9, reps=20):
+    """Interleaved A/B of the fold variants.  As in prefix_ab, every round draws a fresh
+    buffer layout (each buffer a random number of 4 KiB pages into its allocation) and
+    the variants are timed on it; reports the median and range over layouts."""
+    import random
     import torch
     from sos_amd import _lib as L
     torch.cuda.set_device(0)
     dt, op = L.dtype_id(a.dtype), L.op_id(a.op)
     es = L.dtype_size(dt)
     chunk = a.n // a.P
-    ins = [torch.empty(chunk * es, dtype=torch.uint8, device="cuda") for _ in range(a.P)]
-    for k, b in enumerate(ins):
-        L.fill(dt, 0, 0x5EED, k, b.data_ptr(), chunk)
-    NV = 8
-    outs = {v: torch.empty_like(ins[0]) for v in range(NV)}
+    names = ("u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd")
     lib = L.lib()
-    ptrs = [b.data_ptr() for b in ins]
-    res = {v: [] for v in range(NV)}
+    rng = random.Random(99)
+    res = {v: [] for v in range(len(names))}
+    same = True
+    pages = 64
     for _ in range(rounds):
-        for v in range(NV):
+        bufs = [torch.empty(chunk * es + pages * 4096, dtype=torch.uint8, device="cuda")
+                for _ in range(a.P + 1)]
+        ptrs = [b.data_ptr() + rng.randrange(pages) * 4096 for b in bufs]
+        ins, out = ptrs[:a.P], ptrs[a.P]
+        for k, x in enumerate(ins):
+            L.fill(dt, 0, 0x5EED, k, x, chunk)
+        ref = None
+        for v in range(len(names)):
             lib.sosx_set_fold_variant(v)
             for _ in range(3):
-                L.fold(op, dt, L.ORDER_LINEAR, outs[v].data_ptr(), ptrs, chunk)
+                L.fold(op, dt, L.ORDER_LINEAR, out, ins, chunk)
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
             for _ in range(reps):
-                L.fold(op, dt, L.ORDER_LINEAR, outs[v].data_ptr(), ptrs, chunk)
+                L.fold(op, dt, L.ORDER_LINEAR, out, ins, chunk)
             s1.record()
             torch.cuda.synchronize()
             res[v].append(s0.elapsed_time(s1) / reps)
-    lib.sosx_set_fold_variant(0)
-    same = all(torch.equal(outs[0], outs[v]) for v in range(1, NV))
+            last = bufs[-1].clone()
+            if ref is None:
+                ref = last
+            else:
+                same &= torch.equal(ref, last)
+        lib.sosx_set_fold_variant(0)
+        del bufs, ref, last
     algo = (a.P + 1) * chunk * es
     rows = {}
-    for v, name in enumerate(("u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd")):
-        ms = sorted(res[v])[len(res[v]) // 2]
-        rows[name] = {"median_ms": round(ms, 5), "GBs": round(algo / (ms / 1e3) / 1e9, 1)}
+    for v, name in enumerate(names):
+        ms = sorted(res[v])
+        rows[name] = {"median_ms": round(ms[len(ms) // 2], 5),
+                      "GBs": round(algo / (ms[len(ms) // 2] / 1e3) / 1e9, 1),
+                      "GBs_range": [round(algo / (ms[-1] / 1e3) / 1e9, 1),
+                                    round(algo / (ms[0] / 1e3) / 1e9, 1)]}
     print(json.dumps({"fold_ab": rows, "P": a.P, "chunk": chunk, "bytes": algo,
-                      "variants_bit_identical": same}))
+                      "layouts": rounds, "variants_bit_identical": same}))
 
 
 def prefix_ab(a, rounds=9, reps=20):
