@@ -213,10 +213,10 @@ struct PrefixPtrs {
     void *out[kMaxPrefix];
 };
 
-#ifndef PREFIX_U
-#define PREFIX_U 1
-#endif
-constexpr int kPrefixU = PREFIX_U;  // 16-B vectors per lane per tile
+// 16-B vectors per lane per tile.  U = 2/4/8 and plain loads/stores measured slower over
+// random buffer layouts (profiles/r2_prefix_variants*.txt); they stay as
+// bench variants (sosx_set_prefix_variant).
+constexpr int kPrefixU = 1;
 
 // NT: nontemporal loads/stores (the default); the plain variant is a bench A/B only.
 template <class T, class OP, int NP, int U, bool NT = true>
@@ -290,7 +290,7 @@ using namespace sos;
 namespace {
 
 int g_fold_variant = 0;  // tuning experiments on the 8-input fp32 sum fold (bench A/B)
-int g_prefix_variant = 0;  // same for the 8-input fp32 sum prefix
+int g_prefix_variant = 0;  // same for the fp32 sum prefix, 2..8 inputs
 
 template <class T, class OP, int NP, int ORDER, int U>
 int launch_fold_u(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
@@ -384,17 +384,14 @@ int launch_prefix_u(const PrefixPtrs &p, size_t n, hipStream_t st)
 template <class T, class OP, int NP>
 int launch_prefix_np(const PrefixPtrs &p, size_t n, hipStream_t st)
 {
-    const uintptr_t o = (uintptr_t)p.out[0];
     if constexpr (std::is_same<T, float>::value && std::is_same<OP, OpSum>::value && NP >= 2) {
-        if (g_prefix_variant == 5) return launch_prefix_u<T, OP, NP, 8, true>(p, n, st);
         if (g_prefix_variant == 1) return launch_prefix_u<T, OP, NP, 2, true>(p, n, st);
         if (g_prefix_variant == 2) return launch_prefix_u<T, OP, NP, 4, true>(p, n, st);
         if (g_prefix_variant == 3) return launch_prefix_u<T, OP, NP, 1, false>(p, n, st);
         if (g_prefix_variant == 4) return launch_prefix_u<T, OP, NP, 2, false>(p, n, st);
+        if (g_prefix_variant == 5) return launch_prefix_u<T, OP, NP, 8, true>(p, n, st);
     }
-    Geom g = make_geom(o, n, sizeof(T), kPrefixU);
-    hipLaunchKernelGGL((k_prefix<T, OP, NP, kPrefixU>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st, p, g);
-    return hip_ok(hipGetLastError());
+    return launch_prefix_u<T, OP, NP, kPrefixU, true>(p, n, st);
 }
 
 struct PrefixFn {
