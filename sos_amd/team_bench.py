@@ -91,7 +91,6 @@ def main(args, torch):
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank)) % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local)
     dt = L.dtype_id(args.dtype)
     es = L.dtype_size(dt)
     n = args.n
@@ -120,6 +119,9 @@ def main(args, torch):
             os.environ["SHMEMX_TRANSPORT"] = "p2p" if p2p_any else "rccl"
     if rank == 0 and DISABLED:
         log(f"[team] preflight: transports {sorted(DISABLED)} disabled ({pre['why']})")
+    # the device is opened only now: during the preflight the child PE job is the only
+    # process on each GPU (counting devices above does not initialise the runtime)
+    torch.cuda.set_device(local)
     S.shmem_init()
     assert S.shmem_n_pes() == world and S.shmem_my_pe() == rank
     alg = L.ALGS[args.alg]
@@ -794,7 +796,6 @@ def preflight_child():
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank)) % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local)
     os.environ.setdefault("SHMEMX_DEVICE", str(local))
     S.shmem_init()
     dt = L.dtype_id("float")
