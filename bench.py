@@ -18,7 +18,7 @@ HBM bytes per launch / its HIP-event-timed mean duration; `cpu_baseline` is the 
 restatement of reduce_local (oracle/sos_oracle.c, gcc -O2, one core) on a bounded
 sample of the same workload.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--variants] [--no-cpu]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--sweep]
        torchrun --nproc-per-node N bench.py --gpus N   (N > 1)
 """
 import argparse
@@ -53,9 +53,6 @@ def parse():
     p.add_argument("--dtype", default="float")
     p.add_argument("--op", default="sum")
     p.add_argument("--alg", default=os.environ.get("SHMEM_REDUCE_ALGORITHM", "auto"))
-    p.add_argument("--variant", type=int, default=0, help="combine kernel variant")
-    p.add_argument("--variants", action="store_true", help="A/B every combine variant")
-    p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-pmc", action="store_true")
@@ -74,6 +71,12 @@ def parse():
                    help="largest nreduce of the N=1 sweep and of the N>1 size curve")
     p.add_argument("--no-team-sweep", action="store_true",
                    help="N>1: skip the nreduce 1Mi..256Mi size curve")
+    p.add_argument("--no-curve", action="store_true",
+                   help="N=1: skip the nreduce 1Mi..256Mi combine curve (with its CPU column)")
+    p.add_argument("--pmc-save", default=None,
+                   help="N=1: also copy the raw PMC CSVs into this directory")
+    p.add_argument("--fold-p", type=int, default=8,
+                   help="inputs of the fold / prefix kernel legs (one PE's chunk of a P-PE call)")
     p.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args()
     a.n = a.nreduce
@@ -105,19 +108,21 @@ def run_combine(args, torch):
     stream = torch.cuda.current_stream()
     S = stream.cuda_stream
     L, dt, es, a, b = combine_setup(args, torch, S)
-    lib = L.lib()
     op = L.op_id(args.op)
-    lib.sosx_set_combine_variant(args.variant)
     launch = lambda: L.combine(op, dt, a.data_ptr(), b.data_ptr(), args.n, S)  # noqa: E731
 
-    if args.child_pmc:  # profiled child: a few launches only
+    if args.child_pmc:  # profiled child: a few launches of each measured kernel only
         for _ in range(args.warmup + args.steps):
             launch()
         torch.cuda.synchronize()
+        del a, b
+        for kind in ("fold", "prefix"):
+            ms_launch, _, _, keep = multi_stream_setup(args, torch, kind)
+            for _ in range(args.warmup + args.steps):
+                ms_launch()
+            torch.cuda.synchronize()
+            del keep
         return None
-
-    if args.variants:
-        variants_ab(args, torch, L, launch)
 
     for _ in range(args.warmup):
         launch()
@@ -165,8 +170,7 @@ def run_combine(args, torch):
         "data": "synthetic (splitmix64 counter hash, SURVEY.md 8(d)), resident in HBM",
         "config": {"workload": f"shmem_{args.dtype}_{args.op}_reduce local combine "
                                f"(reduce_local inout OP= in), nreduce={args.n}, 1 PE",
-                   "nreduce": args.n, "op": args.op, "type": args.dtype,
-                   "kernel_variant": lib.sosx_combine_variant_name(args.variant).decode()},
+                   "nreduce": args.n, "op": args.op, "type": args.dtype},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None,
@@ -228,81 +232,59 @@ def host_resident(args, torch):
     return out
 
 
-def prefix_kernel(args, torch):
-    """The team scans' local step (sosx_prefix, plan.h PREFIX) at the headline size: P=8
-    input chunks of nreduce/8 elements (one PE's share of an 8-PE scan), 8 outputs.
-    Algorithmic HBM bytes = 2 * P * chunk * sizeof(T).  Reported beside `value`."""
+def multi_stream_setup(args, torch, kind):
+    """P resident input chunks of nreduce/P elements (one PE's share of a P-PE team call)
+    and the launch of the team path's local step on them:
+      fold   : sosx_fold LINEAR (the ring's fused P-way combine), 1 output,
+               algorithmic HBM bytes (P + 1) * chunk * sizeof(T);
+      prefix : sosx_prefix (the scans' local step), P outputs, 2 * P * chunk * sizeof(T)."""
     from sos_amd import _lib as L
+    P = args.fold_p     # default 8: one PE's chunk of an 8-PE call, the 8-GPU node's shape
     dt = L.dtype_id(args.dtype)
     es = L.dtype_size(dt)
-    P = 8
     chunk = args.n // P
-    stream = torch.cuda.current_stream()
-    S = stream.cuda_stream
+    S = torch.cuda.current_stream().cuda_stream
+    dist = L.DIST_PROD if args.op == "prod" else L.DIST_UNIFORM
     ins = [torch.empty(chunk * es, dtype=torch.uint8, device="cuda") for _ in range(P)]
-    outs = [torch.empty_like(x) for x in ins]
+    outs = [torch.empty_like(x) for x in ins[:P if kind == "prefix" else 1]]
     for k, x in enumerate(ins):
-        L.fill(dt, L.DIST_UNIFORM, SEED, k, x.data_ptr(), chunk, 0, S)
+        L.fill(dt, dist, SEED, k, x.data_ptr(), chunk, 0, S)
     ip, op_ = [x.data_ptr() for x in ins], [x.data_ptr() for x in outs]
-    launch = lambda: L.prefix("sum", dt, op_, ip, chunk, -1, S)  # noqa: E731
-    for _ in range(3):
-        launch()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(max(args.steps // 2, 5))]
-    for st_, en in ev:
-        st_.record(stream)
-        launch()
-        en.record(stream)
-    torch.cuda.synchronize()
-    ms = sorted(a.elapsed_time(b) for a, b in ev)
-    mean_s = sum(ms) / len(ms) / 1e3
-    algo = 2 * P * chunk * es
-    del ins, outs
-    return {"kernel": "sos::k_prefix<NP=8>", "inputs": P, "elements_per_input": chunk,
-            "algorithmic_bytes_per_launch": algo, "mean_kernel_ms": round(mean_s * 1e3, 5),
-            "achieved_GBs": round(algo / mean_s / 1e9, 1),
-            "frac_of_hbm_peak": round(algo / mean_s / 1e9 / HBM_PEAK_GBS, 4)}
+    if kind == "prefix":
+        launch = lambda: L.prefix("sum", dt, op_, ip, chunk, -1, S)  # noqa: E731
+        algo = 2 * P * chunk * es
+    else:
+        launch = lambda: L.fold(args.op, dt, L.ORDER_LINEAR, op_[0], ip, chunk, S)  # noqa: E731
+        algo = (P + 1) * chunk * es
+    return launch, algo, chunk, (ins, outs)
 
 
-def variants_ab(args, torch, L, launch):
-    """Interleaved A/B of every combine variant in one process (guide rule 24)."""
-    lib = L.lib()
-    nv = lib.sosx_num_combine_variants()
+def multi_stream_kernel(args, torch, kind):
+    """One of the team path's multi-stream kernels at the headline size (see
+    multi_stream_setup), timed like `roofline`: two HIP events around a batch of
+    back-to-back launches on the stream they run on.  Reported beside `value`; `traffic`
+    is filled from the PMC passes."""
+    launch, algo, chunk, keep = multi_stream_setup(args, torch, kind)
     stream = torch.cuda.current_stream()
-    es = L.dtype_size(L.dtype_id(args.dtype))
-    results = {v: [] for v in range(nv)}
-    for r in range(args.rounds):
-        for v in range(nv):
-            lib.sosx_set_combine_variant(v)
-            for _ in range(3):
-                launch()
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record(stream)
-            for _ in range(20):
-                launch()
-            e.record(stream)
-            torch.cuda.synchronize()
-            results[v].append(s.elapsed_time(e) / 20)
-    log(f"{'variant':>18} {'median ms':>10} {'min ms':>9} {'HBM GB/s(3 streams)':>20}")
-    for v in range(nv):
-        ms = sorted(results[v])
-        med = ms[len(ms) // 2]
-        gbs = 3 * args.n * es / (med / 1e3) / 1e9
-        log(f"{lib.sosx_combine_variant_name(v).decode():>18} {med:10.4f} {ms[0]:9.4f} {gbs:20.1f}")
-    lib.sosx_set_combine_variant(args.variant)
-    # calibration: the runtime's device-to-device copy of the same bytes (2 streams)
-    a = torch.empty(args.n * es, dtype=torch.uint8, device="cuda")
-    b = torch.empty_like(a)
     for _ in range(3):
-        b.copy_(a)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record(stream)
-    for _ in range(20):
-        b.copy_(a)
-    e.record(stream)
+        launch()
+    reps = max(args.steps // 2, 10)
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / 20
-    log(f"{'calib: D2D copy':>18} {ms:10.4f} {'':9} {2 * args.n * es / (ms / 1e3) / 1e9:20.1f}")
+    s0.record(stream)
+    for _ in range(reps):
+        launch()
+    s1.record(stream)
+    torch.cuda.synchronize()
+    mean_s = s0.elapsed_time(s1) / reps / 1e3
+    del keep
+    P = args.fold_p
+    name = {"prefix": f"sos::k_prefix<NP={P}>", "fold": f"sos::k_fold<NP={P}, LINEAR>"}[kind]
+    return {"kernel": name, "inputs": P, "elements_per_input": chunk,
+            "algorithmic_bytes_per_launch": algo, "mean_kernel_ms": round(mean_s * 1e3, 5),
+            "mean_kernel_ms_how": f"HIP-event span of {reps} back-to-back launches / {reps}",
+            "achieved_GBs": round(algo / mean_s / 1e9, 1),
+            "frac_of_hbm_peak": round(algo / mean_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None}
 
 
 # config #5 (and #2, #3): (type, op) pairs of the roofline scan
@@ -396,11 +378,24 @@ def sweep(args, torch):
 # ----------------------------------------------------------------------------------
 # PMC traffic: rocprofv3 --pmc pass(es) over a child run of this script
 # ----------------------------------------------------------------------------------
-def pmc_traffic(args):
-    """HBM bytes per combine launch from TCC FETCH_SIZE/WRITE_SIZE (KB units).
-    gfx950: FETCH_SIZE counts half the bytes of a 16-B/lane streaming read
+PMC_KERNELS = {"combine": "sos::k_combine3<", "fold": "sos::k_fold<", "prefix": "sos::k_prefix<"}
+
+
+def pmc_kernel_of(name):
+    """Which measured kernel (PMC_KERNELS key) a rocprof Kernel_Name belongs to, or None."""
+    for k, tag in PMC_KERNELS.items():
+        if tag in name:
+            return k
+    return None
+
+
+def pmc_traffic(args, save_dir=None):
+    """HBM bytes per launch of each measured kernel (combine, fold, prefix) from TCC
+    FETCH_SIZE / WRITE_SIZE (KiB units), one rocprofv3 --pmc pass per counter over a
+    child run of this script (--child-pmc: a few launches of each kernel at the bench
+    shapes).  gfx950: FETCH_SIZE counts half the bytes of a 16-B/lane streaming read
     (MI355X_MICROARCH.md, HBM), so reads = 2*FETCH_SIZE.  Separate passes, since
-    FETCH_SIZE and WRITE_SIZE do not fit one TCC pass."""
+    FETCH_SIZE and WRITE_SIZE do not fit one TCC pass.  Returns ({kernel: bytes}, info)."""
     prof = shutil.which("rocprofv3")
     if not prof:
         return None, "rocprofv3 not found"
@@ -410,23 +405,33 @@ def pmc_traffic(args):
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--child-pmc", "--steps", "3",
                "--warmup", "1", "--nreduce", str(args.n), "--dtype", args.dtype, "--op", args.op,
-               "--variant", str(args.variant)]
+               "--fold-p", str(args.fold_p)]
         try:
+            env = {k: v for k, v in os.environ.items()
+                   if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                "GROUP_RANK", "ROLE_RANK")}   # the child is one process
             subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL,
-                           stderr=subprocess.DEVNULL, env=dict(os.environ, TMPDIR="/tmp"))
+                           stderr=subprocess.DEVNULL, env=dict(env, TMPDIR="/tmp"))
         except Exception as exc:  # noqa: BLE001 - a profiler failure must not kill the bench
+            shutil.rmtree(d, ignore_errors=True)
             return None, f"rocprofv3 {ctr} pass failed: {exc}"
-        rows = []
+        rows = {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+            if save_dir:
+                os.makedirs(save_dir, exist_ok=True)
+                shutil.copy(f, os.path.join(save_dir, f"pmc_{ctr}.csv"))
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if "k_combine3" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
-                        rows.append(float(row["Counter_Value"]))
+                    k = pmc_kernel_of(row.get("Kernel_Name", ""))
+                    if k and row.get("Counter_Name") == ctr:
+                        rows.setdefault(k, []).append(float(row["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not rows:
             return None, f"no {ctr} rows"
-        vals[ctr] = sum(rows) / len(rows)
-    traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+        for k, v in rows.items():
+            vals.setdefault(k, {})[ctr] = sum(v) / len(v)
+    traffic = {k: (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0
+               for k, v in vals.items() if len(v) == 2}
     return traffic, vals
 
 
@@ -461,6 +466,73 @@ def cpu_baseline(args):
                       f"host: {model}, nproc={os.cpu_count()}"}
 
 
+CURVE_SIZES = (1 << 20, 4 << 20, 16 << 20, 64 << 20, 128 << 20, 256 << 20)
+
+
+def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
+    """The north star's N = 1 curve: the device combine (sosx_combine) at nreduce =
+    1Mi .. 256Mi, each point with the mean HIP-event kernel time over a batch of
+    back-to-back launches, HBM GB/s (3 * n * s per launch) and its fraction of peak,
+    payload GiB/s, and beside it SOS's own CPU reduce_local (the oracle restatement of
+    src/shmem_internal_op.h:23-33,305-339, gcc -O2, 1 pinned thread) on the same inputs,
+    timed for about `cpu_seconds` per point.  Points <= 16Mi keep their three streams in
+    the 256 MiB Infinity Cache between launches, so they read above the HBM rate (and
+    the CPU's 1Mi point runs from its own caches)."""
+    from sos_amd import _lib as L
+    O = None
+    if cpu:
+        from oracle import oracle as O
+    dt, op = L.dtype_id(args.dtype), L.op_id(args.op)
+    es = L.dtype_size(dt)
+    dist = L.DIST_PROD if args.op == "prod" else L.DIST_UNIFORM
+    stream = torch.cuda.current_stream()
+    S = stream.cuda_stream
+    sizes = [m for m in CURVE_SIZES if m <= args.sweep_max]
+    nmax = max(sizes)
+    a = torch.empty(nmax * es, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    rows = []
+    for m in sizes:
+        L.fill(dt, dist, SEED, 0, a.data_ptr(), m, 0, S)
+        L.fill(dt, dist, SEED, 1, b.data_ptr(), m, 0, S)
+        launch = lambda: L.combine(op, dt, a.data_ptr(), b.data_ptr(), m, S)  # noqa: E731
+        for _ in range(3):
+            launch()
+        reps = max(10, min(200, int(4e9 // (3 * m * es))))
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s0.record(stream)
+        for _ in range(reps):
+            launch()
+        s1.record(stream)
+        torch.cuda.synchronize()
+        kern = s0.elapsed_time(s1) / 1e3 / reps
+        algo = 3 * m * es
+        row = {"nreduce": m, "kernel_us": round(kern * 1e6, 2),
+               "GBs": round(algo / kern / 1e9, 1),
+               "frac_hbm": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4),
+               "gpu_GiBs": round(m * es / kern / GiB, 2)}
+        if O is not None:
+            inout = O.fill(dt, dist, SEED, 0, m)
+            inp = O.fill(dt, dist, SEED, 1, m)
+            t1 = O.time_reduce_local(op, dt, inp, inout, 1)
+            creps = max(1, int(cpu_seconds / max(t1, 1e-6)))
+            t = O.time_reduce_local(op, dt, inp, inout, creps)
+            row["cpu_GiBs"] = round(creps * m * es / t / GiB, 3)
+            row["cpu_reps"] = creps
+            row["gpu_over_cpu"] = round(row["gpu_GiBs"] / row["cpu_GiBs"], 1)
+            del inout, inp
+        rows.append(row)
+        log(f"[curve] n={m:>10} {row['kernel_us']:10.2f} us {row['GBs']:8.1f} GB/s "
+            f"frac {row['frac_hbm']:.3f}  cpu {row.get('cpu_GiBs')} GiB/s")
+    del a, b
+    return {"op": args.op, "type": args.dtype, "kernel": "sos::k_combine3",
+            "gpu": "mean HIP-event kernel time over a batch of back-to-back launches",
+            "cpu": (f"oracle/sos_oracle.c reduce_local (SOS's loop, gcc -O2), 1 thread, "
+                    f"~{cpu_seconds:g} s per point, same inputs" if cpu else "skipped"),
+            "rows": rows}
+
+
 # ----------------------------------------------------------------------------------
 def main():
     args = parse()
@@ -469,9 +541,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus and not args.child_pmc:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    if world > 1 or args.team:
-        from sos_amd import team_bench
-        return team_bench.main(args, torch)
+    if (world > 1 or args.team) and not args.child_pmc:
+        sys.path.insert(0, os.path.join(HERE, "tools"))
+        import team_bench   # the N > 1 leg (bench code: tools/team_bench.py)
+        return team_bench.main(args, torch, pmc=pmc_traffic)
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     if args.sweep:
         print(json.dumps(sweep(args, torch)), flush=True)
@@ -479,18 +552,29 @@ def main():
     res = run_combine(args, torch)
     if res is None:
         return 0
+    if rank == 0 and not args.no_adjacent:
+        res["fold_kernel"] = multi_stream_kernel(args, torch, "fold")
+        res["scan_prefix_kernel"] = multi_stream_kernel(args, torch, "prefix")
     if rank == 0 and not args.no_pmc:
-        traffic, info = pmc_traffic(args)
-        if traffic is not None:
-            res["roofline"]["traffic"] = round(traffic)
-            res["roofline"]["traffic_note"] = ("(2*FETCH_SIZE + WRITE_SIZE)*1024 B per launch, "
-                                               "rocprofv3 --pmc, gfx950 FETCH_SIZE halving corrected")
+        traffic, info = pmc_traffic(args, save_dir=args.pmc_save)
+        note = ("(2*FETCH_SIZE + WRITE_SIZE)*1024 B per launch, rocprofv3 --pmc (one pass "
+                "per counter), gfx950 FETCH_SIZE halving corrected")
+        if traffic is not None and "combine" in traffic:
+            res["roofline"]["traffic"] = round(traffic["combine"])
+            res["roofline"]["traffic_note"] = note
+            res["roofline"]["traffic_over_algorithmic"] = round(
+                traffic["combine"] / res["roofline"]["algorithmic_bytes_per_launch"], 5)
+            for kind, key in (("fold", "fold_kernel"), ("prefix", "scan_prefix_kernel")):
+                if key in res and kind in traffic:
+                    res[key]["traffic"] = round(traffic[kind])
+                    res[key]["traffic_over_algorithmic"] = round(
+                        traffic[kind] / res[key]["algorithmic_bytes_per_launch"], 5)
         else:
             res["roofline"]["traffic_note"] = str(info)
     if rank == 0 and not args.no_host:
         res["host_resident"] = host_resident(args, torch)
-    if rank == 0 and not args.no_adjacent:
-        res["scan_prefix_kernel"] = prefix_kernel(args, torch)
+    if rank == 0 and not args.no_curve:
+        res["size_curve"] = size_curve_n1(args, torch, cpu=not args.no_cpu)
     if rank == 0 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(res), flush=True)

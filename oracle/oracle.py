@@ -57,6 +57,11 @@ def lib():
         L.oracle_pe_ring_time.argtypes = [vp, sz, i, i, sz, i, i, vp, i,
                                           ctypes.POINTER(ctypes.c_long)]
         L.oracle_pe_ring_time.restype = ctypes.c_double
+        L.oracle_pe_recdbl.argtypes = [vp, sz, i, i, sz, i, i, vp]
+        L.oracle_pe_recdbl.restype = i
+        L.oracle_pe_time.argtypes = [i, vp, sz, i, i, sz, i, i, vp, i,
+                                     ctypes.POINTER(ctypes.c_long)]
+        L.oracle_pe_time.restype = ctypes.c_double
         _L = L
     return _L
 
@@ -139,14 +144,18 @@ def time_reduce_local(op, dt, inp, inout, reps):
 
 
 class PeRing:
-    """One PE of SOS's ring run by a real process (oracle_pe_ring): the N > 1 CPU
-    baseline.  Every PE process maps the same shared segment `path` (PE 0 creates it
-    before the others open it; the caller provides that ordering) holding every PE's
-    pSync words and target; the source stays private to the process."""
+    """One PE of SOS's ring (alg "ring", oracle_pe_ring: the N > 1 CPU baseline) or
+    recdbl_sw (alg "recdbl", oracle_pe_recdbl: the small-message latency comparison) run
+    by a real process.  Every PE process maps the same shared segment `path` (PE 0
+    creates it before the others open it; the caller provides that ordering) holding
+    every PE's pSync words and target; the source stays private to the process."""
 
-    def __init__(self, path, P, me, count, dt, create):
+    ALGS = {"ring": 0, "recdbl": 1}
+
+    def __init__(self, path, P, me, count, dt, create, alg="ring"):
         import mmap
         self.P, self.me, self.count, self.dt = P, me, count, dt
+        self.alg = self.ALGS[alg]
         ts = lib().oracle_type_size(dt)
         self.stride = (count * ts + 4095) & ~4095
         self.hdr = lib().oracle_pe_header_bytes(P)
@@ -174,16 +183,16 @@ class PeRing:
         lib().oracle_pe_barrier(self.base, self.P, self.epoch.value)
 
     def run(self, op, src):
-        rc = lib().oracle_pe_ring(self.base, self.stride, self.P, self.me, self.count, op, self.dt,
-                                  _ptr(src))
+        fn = lib().oracle_pe_recdbl if self.alg == 1 else lib().oracle_pe_ring
+        rc = fn(self.base, self.stride, self.P, self.me, self.count, op, self.dt, _ptr(src))
         if rc:
-            raise ValueError(f"oracle_pe_ring rc={rc}")
+            raise ValueError(f"oracle_pe_{'recdbl' if self.alg else 'ring'} rc={rc}")
 
     def time(self, op, src, reps):
-        t = lib().oracle_pe_ring_time(self.base, self.stride, self.P, self.me, self.count, op,
-                                      self.dt, _ptr(src), reps, ctypes.byref(self.epoch))
+        t = lib().oracle_pe_time(self.alg, self.base, self.stride, self.P, self.me, self.count,
+                                 op, self.dt, _ptr(src), reps, ctypes.byref(self.epoch))
         if t < 0:
-            raise ValueError("oracle_pe_ring failed")
+            raise ValueError("oracle_pe_time failed")
         return t
 
     def close(self):

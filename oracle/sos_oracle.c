@@ -393,16 +393,18 @@ int oracle_fill(int dt, int dist, uint64_t seed, int pe, void *dst, size_t count
  * (never the target, so the in-place tmp copy of :672-683 does not arise).
  * ------------------------------------------------------------------------------ */
 #define PE_LINE 64
+#define PE_SYNC 35   /* SHMEM_REDUCE_SYNC_SIZE words per PE (configure.ac:653-694) */
 
 size_t oracle_pe_header_bytes(int P)
 {
-    size_t h = (size_t) (1 + 2 * P) * PE_LINE;
+    size_t h = (size_t) (1 + PE_SYNC * P) * PE_LINE;
     return (h + 4095) & ~(size_t) 4095;
 }
 
+/* PE pe's pSync[k], one 64-B line per word so spinning PEs do not share lines */
 static long *pe_psync(void *seg, int pe, int k)
 {
-    return (long *) ((uint8_t *) seg + (size_t) (1 + 2 * pe + k) * PE_LINE);
+    return (long *) ((uint8_t *) seg + (size_t) (1 + PE_SYNC * pe + k) * PE_LINE);
 }
 
 static void pe_wait_ge(long *p, long v)
@@ -456,15 +458,104 @@ int oracle_pe_ring(void *seg, size_t stride, int P, int me, size_t count, int op
     return rc;
 }
 
-/* `reps` ring calls, each preceded by a barrier (the team API's pSync slot reuse rule,
- * src/shmem_team.c:540-585); barrier epochs continue from *epoch.  Returns seconds. */
-double oracle_pe_ring_time(void *seg, size_t stride, int P, int me, size_t count, int op, int dt,
-                           const void *source, int reps, long *epoch)
+/* ------------------------------------------------------------------------------
+ * One PE of SOS's recdbl_sw (src/collectives.c:850-984) run by a real process: the CPU
+ * side of the small-message latency comparison (SOS AUTO below COLL_SIZE_CROSSOVER,
+ * src/shmem_collectives.h:192-195).  Same segment layout as oracle_pe_ring.  Puts are
+ * memcpy into the peer's target + release fence; put_scalar of the ready flags is an
+ * atomic store into the peer's pSync word; SHMEM_WAIT_UNTIL(.., CMP_EQ, v) spins on the
+ * PE's own word.  current_target is malloc'd per call, as in the reference (:860).
+ * pSync words: [i] step i (:933), [33] the extra-peer word (:862), all reset at :982.
+ * ------------------------------------------------------------------------------ */
+static void pe_wait_eq(long *p, long v)
+{
+    while (__atomic_load_n(p, __ATOMIC_ACQUIRE) != v) __builtin_ia32_pause();
+}
+
+int oracle_pe_recdbl(void *seg, size_t stride, int P, int me, size_t count, int op, int dt,
+                     const void *source)
+{
+    size_t ts = oracle_type_size(dt);
+    if (!ts || me < 0 || me >= P) return -1;
+    uint8_t *base = (uint8_t *) seg + oracle_pe_header_bytes(P);
+    uint8_t *target = base + (size_t) me * stride;
+    const size_t wrk = count * ts;
+    const long target_ready = 1, data_ready = 2;
+    if (P == 1) { if (count) memcpy(target, source, wrk); return 0; }   /* :865-871 */
+    if (count == 0) return 0;                                          /* :873-876 */
+    int log2p = 1, pow2 = 2, i = P >> 1;
+    while (i != 1) { i >>= 1; pow2 <<= 1; log2p++; }                   /* :878-882 */
+    uint8_t *cur = malloc(wrk);                                        /* :860, :888 */
+    if (!cur) return -1;
+    memcpy(cur, source, wrk);
+    long *extra = pe_psync(seg, me, PE_SYNC - 2);                      /* :862 */
+    int rc = 0;
+    if (me >= pow2) {                                                  /* :905-918 */
+        int peer = me - pow2;
+        pe_wait_eq(extra, target_ready);
+        memcpy(base + (size_t) peer * stride, cur, wrk);
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        __atomic_store_n(pe_psync(seg, peer, PE_SYNC - 2), data_ready, __ATOMIC_RELEASE);
+        pe_wait_eq(extra, data_ready);
+    } else {
+        if (me < P - pow2) {                                           /* :920-926 */
+            int peer = me + pow2;
+            __atomic_store_n(pe_psync(seg, peer, PE_SYNC - 2), target_ready, __ATOMIC_RELEASE);
+            pe_wait_eq(extra, data_ready);
+            rc |= oracle_reduce_local(op, dt, (int) count, target, cur);
+        }
+        for (i = 0; i < log2p; i++) {                                  /* :932-963 */
+            long *step = pe_psync(seg, me, i);
+            int peer = me ^ (1 << i);
+            long *peer_step = pe_psync(seg, peer, i);
+            uint8_t *peer_target = base + (size_t) peer * stride;
+            if (me < peer) {
+                __atomic_store_n(peer_step, target_ready, __ATOMIC_RELEASE);
+                pe_wait_eq(step, data_ready);
+                memcpy(peer_target, cur, wrk);
+                __atomic_thread_fence(__ATOMIC_RELEASE);
+                __atomic_store_n(peer_step, data_ready, __ATOMIC_RELEASE);
+            } else {
+                pe_wait_eq(step, target_ready);
+                memcpy(peer_target, cur, wrk);
+                __atomic_thread_fence(__ATOMIC_RELEASE);
+                __atomic_store_n(peer_step, data_ready, __ATOMIC_RELEASE);
+                pe_wait_eq(step, data_ready);
+            }
+            rc |= oracle_reduce_local(op, dt, (int) count, target, cur);  /* :961-962 */
+        }
+        if (me < P - pow2) {                                           /* :966-975 */
+            int peer = me + pow2;
+            memcpy(base + (size_t) peer * stride, cur, wrk);
+            __atomic_thread_fence(__ATOMIC_RELEASE);
+            __atomic_store_n(pe_psync(seg, peer, PE_SYNC - 2), data_ready, __ATOMIC_RELEASE);
+        }
+        memcpy(target, cur, wrk);                                      /* :977 */
+    }
+    free(cur);
+    for (i = 0; i < PE_SYNC; i++)                                      /* :982-983 */
+        __atomic_store_n(pe_psync(seg, me, i), 0, __ATOMIC_RELEASE);
+    return rc;
+}
+
+/* `reps` calls of the ring (alg 0) or recdbl_sw (alg 1), each preceded by a barrier (the
+ * team API's pSync slot reuse rule, src/shmem_team.c:540-585); barrier epochs continue
+ * from *epoch.  Returns seconds. */
+double oracle_pe_time(int alg, void *seg, size_t stride, int P, int me, size_t count, int op,
+                      int dt, const void *source, int reps, long *epoch)
 {
     double t0 = now_s();
     for (int r = 0; r < reps; r++) {
         oracle_pe_barrier(seg, P, ++*epoch);
-        if (oracle_pe_ring(seg, stride, P, me, count, op, dt, source)) return -1.0;
+        int rc = alg == 1 ? oracle_pe_recdbl(seg, stride, P, me, count, op, dt, source)
+                          : oracle_pe_ring(seg, stride, P, me, count, op, dt, source);
+        if (rc) return -1.0;
     }
     return now_s() - t0;
+}
+
+double oracle_pe_ring_time(void *seg, size_t stride, int P, int me, size_t count, int op, int dt,
+                           const void *source, int reps, long *epoch)
+{
+    return oracle_pe_time(0, seg, stride, P, me, count, op, dt, source, reps, epoch);
 }

@@ -1,10 +1,12 @@
-"""CPU: the multi-process ring PE (oracle_pe_ring), bench.py's N > 1 CPU baseline.
+"""CPU: the multi-process PEs of the oracle -- oracle_pe_ring (bench.py's N > 1 CPU
+baseline) and oracle_pe_recdbl (the small-message latency comparison).
 
-P real processes, one per PE, run SOS's ring (src/collectives.c:647-764) over one
-shared segment (memcpy puts + atomic pSync adds, as XPMEM).  Every PE's target must
-equal the single-process ring simulation (oracle_ring) bit for bit: same chunk math,
-same in/inout roles.  Repeated calls through the timing entry (barrier per call) must
-leave the same result, and the pSync words back at SHMEM_SYNC_VALUE (0).
+P real processes, one per PE, run SOS's ring (src/collectives.c:647-764) or recdbl_sw
+(:850-984) over one shared segment (memcpy puts + atomic pSync adds / flag stores, as
+XPMEM).  Every PE's target must equal the single-process simulation (oracle_ring /
+oracle_recdbl) bit for bit: same chunk math, same in/inout roles, same per-PE tree.
+Repeated calls through the timing entry (barrier per call) must leave the same
+result, and the pSync words back at SHMEM_SYNC_VALUE (0).
 """
 import multiprocessing as mp
 import os
@@ -18,9 +20,9 @@ FLOAT, DOUBLE, INT64, INT = 23, 24, 11, 4
 SUM, PROD, BXOR, MAX = 5, 6, 2, 4
 
 
-def _pe(path, P, me, count, dt, op, dist, reps, q):
+def _pe(path, P, me, count, dt, op, dist, reps, q, alg):
     try:
-        ring = O.PeRing(path, P, me, count, dt, create=False)
+        ring = O.PeRing(path, P, me, count, dt, create=False, alg=alg)
         src = O.fill(dt, dist, 0x5EED, me, count)
         ring.barrier()  # every PE mapped
         if reps:
@@ -36,6 +38,7 @@ def _pe(path, P, me, count, dt, op, dist, reps, q):
         q.put((me, repr(e)))
 
 
+@pytest.mark.parametrize("alg", ["ring", "recdbl"])
 @pytest.mark.parametrize("P,count,dt,op,dist,reps", [
     (2, 1001, FLOAT, SUM, 0, 0),
     (3, 4097, DOUBLE, PROD, 1, 0),
@@ -44,13 +47,13 @@ def _pe(path, P, me, count, dt, op, dist, reps, q):
     (8, 12345, INT, MAX, 0, 2),
     (3, 2, DOUBLE, SUM, 0, 0),   # fewer elements than PEs: empty chunks
 ])
-def test_pe_ring_matches_simulated_ring(tmp_path, P, count, dt, op, dist, reps):
-    path = f"/dev/shm/sosx_pe_ring_test_{os.getpid()}_{P}_{count}"
-    owner = O.PeRing(path, P, 0, count, dt, create=True)
+def test_pe_matches_simulated_schedule(tmp_path, P, count, dt, op, dist, reps, alg):
+    path = f"/dev/shm/sosx_pe_{alg}_test_{os.getpid()}_{P}_{count}"
+    owner = O.PeRing(path, P, 0, count, dt, create=True, alg=alg)
     try:
         ctx = mp.get_context("fork")
         q = ctx.Queue()
-        procs = [ctx.Process(target=_pe, args=(path, P, me, count, dt, op, dist, reps, q))
+        procs = [ctx.Process(target=_pe, args=(path, P, me, count, dt, op, dist, reps, q, alg))
                  for me in range(P)]
         for p in procs:
             p.start()
@@ -59,12 +62,12 @@ def test_pe_ring_matches_simulated_ring(tmp_path, P, count, dt, op, dist, reps):
             p.join(timeout=60)
             assert p.exitcode == 0
         srcs = [O.fill(dt, dist, 0x5EED, me, count) for me in range(P)]
-        exp = O.ring(op, dt, srcs)
+        exp = (O.ring if alg == "ring" else O.recdbl)(op, dt, srcs)
         for me in range(P):
             assert isinstance(got[me], bytes), got[me]
-            assert got[me] == exp[me].tobytes(), f"PE {me} differs from oracle_ring"
+            assert got[me] == exp[me].tobytes(), f"PE {me} differs from oracle_{alg}"
         words = np.frombuffer(owner.mm, dtype=np.int64, count=owner.hdr // 8)
-        assert not words[8:8 * (1 + 2 * P)].any(), "pSync words not restored to 0"
+        assert not words[8:].any(), "pSync words not restored to 0"
         del words
     finally:
         owner.close()

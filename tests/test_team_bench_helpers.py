@@ -1,7 +1,12 @@
-"""CPU: the N > 1 bench's transport switching (sos_amd/team_bench.py) against a fake
-library: each measured transport selects the library transport and, for p2p, the
-signalling mode; an unavailable one reports False; reset restores rccl + host mode."""
-from sos_amd import team_bench as TB
+"""CPU: the N > 1 bench's helpers (tools/team_bench.py) against fakes: transport
+switching (each measured transport selects the library transport and, for p2p, the
+signalling mode; an unavailable one reports False; reset restores rccl + stream mode),
+the preflight job's verdicts, and which transport `value` may come from."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+import team_bench as TB  # noqa: E402
 
 
 class _Lib:
@@ -70,7 +75,7 @@ def _run_preflight(monkeypatch, stdout, rc=0, timeout=False):
 
     class FakePopen:
         def __init__(self, cmd, cwd=None, env=None, stdout=None, stderr=None):
-            assert cmd[-3:] == ["-m", "sos_amd.team_bench", "--preflight"]
+            assert cmd[-1] == "--preflight" and cmd[-2].endswith(os.path.join("tools", "team_bench.py"))
             assert env["MASTER_PORT"] == str(29500 + TB.PREFLIGHT_PORT_OFFSET)
             assert env["SHMEMX_P2P_TIMEOUT"] == "20"
             stdout.write(out_text)
@@ -138,3 +143,32 @@ def test_preflight_off(monkeypatch):
     monkeypatch.setenv("SOSX_BENCH_PREFLIGHT", "0")
     pre = TB.preflight(torch, _Dist(), 0, 2)
     assert not pre["ran"] and all(pre["ok"].values())
+
+
+def _res(t_step, mismatches, available=True):
+    return {"t_step": t_step, "mismatches": mismatches, "available": available}
+
+
+def test_value_never_from_rccl_allreduce():
+    """rccl_ar is RCCL's own ncclAllReduce: even clean and fastest it never gives `value`."""
+    results = {"rccl": _res(3.0, 0), "rccl_ag": _res(2.9, 0), "p2p": _res(2.5, 0),
+               "p2p_host": _res(2.7, 0), "rccl_ar": _res(1.0, 0)}
+    assert TB.select_primary(results) == ("p2p", None)
+    results["p2p"] = _res(2.5, 4)          # a failed check is never `value` either
+    assert TB.select_primary(results) == ("p2p_host", None)
+    assert "rccl_ar" not in TB.VALUE_T
+
+
+def test_value_null_when_every_check_fails():
+    results = {"rccl": _res(3.0, 1), "rccl_ag": _res(2.9, 7), "p2p": {"available": False},
+               "p2p_host": {"available": False}, "rccl_ar": _res(1.0, 0)}
+    primary, why = TB.select_primary(results)
+    assert primary is None and "rccl 1" in why and "rccl_ag 7" in why
+    primary, why = TB.select_primary({"rccl_ar": _res(1.0, 0), "p2p": {"available": False}})
+    assert primary is None and "available" in why
+
+
+def test_workload_names_what_ran():
+    assert "ncclAllGather" in TB.workload_text("rccl_ag", "float", "sum", 8, 2)
+    assert "host-signalled" in TB.workload_text("p2p_host", "float", "sum", 8, 2)
+    assert "no valid measurement" in TB.workload_text(None, "float", "sum", 8, 2)

@@ -1,5 +1,8 @@
 """N > 1 leg of bench.py: shmem_<T>_<op>_reduce over one PE per GPU.
 
+Bench code, not product code: it lives in tools/ (it imports the CPU oracle for its
+CPU-baseline leg, which the product package never does).
+
 Launched by torchrun (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).  torch.distributed
 (gloo, CPU) is only the bench's control plane (barrier, max over ranks).  The data path
 is libsos_amd.so behind the public C API: shmem_init() bootstraps over TCP
@@ -15,7 +18,8 @@ Both inter-PE transports are measured (SHMEMX_TRANSPORT=both):
   rccl_ar    : RCCL's own ncclAllReduce (SHMEMX_RCCL_ALLREDUCE=2): the reference point
                for the SOS schedules; for fp sum its bits follow RCCL's order, so it is
                checked against the fp tolerance bound instead and never gives `value`
-`value` is the fastest one whose bitwise check is clean.
+`value` is the fastest of the library's SOS-schedule transports (rccl, rccl_ag, p2p,
+p2p_host) whose bitwise check is clean on every rank; null (with the reason) if none.
 Self-check: after timing, every rank regenerates all P inputs on its own GPU and
 re-evaluates the schedule's element order with the fold kernel (ring: chunk c folded
 from PE c rightwards, src/collectives.c:693-727; tree schedules: the recdbl_sw tree),
@@ -26,6 +30,11 @@ import json
 import os
 import sys
 import time
+
+# bench code, not product code: it lives in tools/ and reaches the package from the repo root
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _ROOT not in sys.path:
+    sys.path.insert(0, _ROOT)
 
 ctypes_u8 = ctypes.c_uint8
 
@@ -48,6 +57,37 @@ T_NAMES = tuple(t[0] for t in TRANSPORTS)
 # the SOS schedules (bit-exact); rccl_ar ignores the schedule, so the schedule, host and
 # scan/broadcast legs skip it (the headline and the size curve measure it)
 SCHEDULE_T = ("rccl", "rccl_ag", "p2p", "p2p_host")
+# the transports `value` may come from: the library's own SOS schedules + HIP fold.
+# rccl_ar is RCCL's ncclAllReduce (no library kernel on the data path): never `value`,
+# even where its bits happen to equal SOS's ring (integer ops, fp sum at P = 2).
+VALUE_T = SCHEDULE_T
+
+
+def select_primary(results):
+    """(transport `value` comes from, None) or (None, reason).  Only a VALUE_T transport
+    that was measured and whose bitwise check is clean on every rank qualifies; there is
+    no fallback to a faster transport whose check failed."""
+    measured = [k for k in VALUE_T if k in results and results[k].get("available", True)]
+    if not measured:
+        return None, "no SOS-schedule transport was available (preflight or bring-up failed)"
+    clean = [k for k in measured if results[k]["mismatches"] == 0]
+    if not clean:
+        return None, ("every SOS-schedule transport failed its bitwise check: "
+                      + ", ".join(f"{k} {results[k]['mismatches']}" for k in measured))
+    return min(clean, key=lambda k: results[k]["t_step"]), None
+
+
+def workload_text(tname, dtype, op, n, world):
+    """config.workload for what actually ran."""
+    head = f"shmem_{dtype}_{op}_reduce(SHMEM_TEAM_WORLD) nreduce={n} per PE, {world} PEs (1 per MI355X), "
+    data_path = {
+        "rccl": "ncclSend/ncclRecv over xGMI + HIP fold kernel",
+        "rccl_ag": "ncclSend/ncclRecv + ncclAllGather over xGMI + HIP fold kernel",
+        "p2p": "p2p reads of IPC-mapped peer HBM + HIP fold kernel, stream-signalled rounds",
+        "p2p_host": "p2p reads of IPC-mapped peer HBM + HIP fold kernel, host-signalled rounds",
+    }
+    return head + data_path.get(tname, "no valid measurement")
+
 
 # transports that failed the preflight on some rank (every leg skips them)
 DISABLED = set()
@@ -83,7 +123,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main(args, torch):
+def main(args, torch, pmc=None):
     import torch.distributed as dist
     from sos_amd import _lib as L
     from sos_amd import shmem as S
@@ -213,14 +253,26 @@ def main(args, torch):
 
     local_leg = local_combine(args, torch, dist, L, dt, es, n, src, dst, stream, world)
 
-    # `value` is the faster transport among those whose bitwise check is clean (both are
-    # the library's: SHMEMX_TRANSPORT=rccl|p2p); every measured transport is reported
+    # HBM traffic of the fold kernel: rank 0 runs bench.py's PMC passes (rocprofv3 --pmc
+    # FETCH_SIZE, then WRITE_SIZE) over a one-process child launching the same kernel at
+    # this call's shape (P inputs of n/P elements) on its GPU; the other ranks wait
+    fold_traffic = None
+    if (pmc is not None and not getattr(args, "no_pmc", False)
+            and os.environ.get("SOSX_BENCH_PMC", "1") != "0"
+            and resolved in (L.ALGS["ring"], L.ALGS["recdbl_direct"])):
+        if rank == 0:
+            log(f"[team] PMC passes over the fold kernel (P = {P}, {n // P} elements per input)")
+            args.fold_p = P
+            tr, info = pmc(args)
+            fold_traffic = tr.get("fold") if tr else None
+            if fold_traffic is None:
+                log(f"[team] PMC: {info}")
+        dist.barrier()
+
+    # every measured transport is reported; `value` only from one of the library's SOS
+    # schedules whose bitwise check is clean (select_primary)
     measured = [k for k in T_NAMES if results[k].get("available", True)]
-    clean = [k for k in measured if results[k]["mismatches"] == 0]
-    primary = min(clean or measured, key=lambda k: results[k]["t_step"])
-    r = results[primary]
-    t_step, prof = r["t_step"], r["prof"]
-    fold_ms = prof["fold_ms"] / max(prof["nfold"], 1)
+    primary, why_null = select_primary(results)
     if resolved in (L.ALGS["ring"], L.ALGS["recdbl_direct"]):
         fold_bytes = (P + 1) * (n // P) * es       # P inputs of one chunk + the output
     else:
@@ -241,47 +293,55 @@ def main(args, torch):
                     "note": "RCCL's own order: compared with the fp bound, not bit for bit"}
                    if "tolerance_violations" in rr else {})}
 
+    r = results[primary] if primary else None
+    t_step = r["t_step"] if r else None
+    fold_ms = r["prof"]["fold_ms"] / max(r["prof"]["nfold"], 1) if r else 0.0
     res = {
         "metric": "GiB/s device-resident sum_reduce combine, nreduce=128Mi fp32; 1/2/4/8 GPU",
-        "value": round(world * n * es / t_step / GiB, 3),
+        "value": round(world * n * es / t_step / GiB, 3) if r else None,
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(t_step * 1e3, 4),
+        "ms_per_step": round(t_step * 1e3, 4) if r else None,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": {"float": "f32", "double": "f64"}.get(args.dtype, args.dtype),
         "data": "synthetic (splitmix64 counter hash per PE, SURVEY.md 8(d)), resident in HBM",
-        "config": {"workload": f"shmem_{args.dtype}_{args.op}_reduce(SHMEM_TEAM_WORLD) nreduce={n} "
-                               f"per PE, {world} PEs (1 per MI355X), "
-                               + ("RCCL over xGMI + HIP fold" if primary.startswith("rccl") else
-                                  "p2p reads of IPC-mapped peer HBM + HIP fold"
-                                  + (", host-signalled rounds" if primary == "p2p_host" else "")),
+        "config": {"workload": workload_text(primary, args.dtype, args.op, n, world),
                    "nreduce": n, "algorithm": name, "transport": primary,
                    "parallelism": f"pe{world}"},
         "roofline": {"bound": "hbm", "kernel": "sos::k_fold (fused P-way combine)",
                      "achieved": round(fold_bytes / (fold_ms / 1e3) / 1e9, 1) if fold_ms > 0 else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(fold_bytes / (fold_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if fold_ms > 0 else None,
-                     "traffic": None, "algorithmic_bytes_per_launch": fold_bytes,
-                     "mean_kernel_ms": round(fold_ms, 5),
+                     "traffic": round(fold_traffic) if fold_traffic else None,
+                     **({"traffic_over_algorithmic": round(fold_traffic / fold_bytes, 5),
+                         "traffic_note": "(2*FETCH_SIZE + WRITE_SIZE)*1024 B per launch, "
+                                         "rocprofv3 --pmc over a one-process child running "
+                                         "this kernel at this shape on GPU 0"}
+                        if fold_traffic else {}),
+                     "algorithmic_bytes_per_launch": fold_bytes,
+                     "mean_kernel_ms": round(fold_ms, 5) if r else None,
                      **({"note": "p2p: the fold reads its P-1 peer inputs in place over xGMI, "
                                  "so this launch is link-bound (see team_roofline)"}
-                        if primary.startswith("p2p") else {})},
-        "team_roofline": dict(bound="xgmi", wire_bytes_per_pe=int(wire), **team_roof(r)),
-        "check": {"bitwise_mismatches_all_ranks": r["mismatches"],
+                        if primary and primary.startswith("p2p") else {})},
+        "team_roofline": dict(bound="xgmi", wire_bytes_per_pe=int(wire), **team_roof(r)) if r else None,
+        "check": {"bitwise_mismatches_all_ranks": r["mismatches"] if r else None,
                   "against": "on-GPU regeneration of all PE inputs + schedule-order fold"},
     }
+    if why_null:
+        res["value_null_reason"] = why_null
     res["transports"] = {k: team_roof(results[k]) for k in measured}
-    res["transport_choice"] = ("value = the faster of the measured transports with a clean "
-                               "bitwise check; the library default is rccl "
+    res["transport_choice"] = ("value = the fastest of the library's SOS-schedule transports "
+                               f"({', '.join(VALUE_T)}) whose bitwise check is clean on every "
+                               "rank, else null; the library default is rccl "
                                "(SHMEMX_TRANSPORT selects; rccl_ag = rccl with "
                                "SHMEMX_RCCL_ALLGATHER=1, p2p_host = p2p with "
-                               "SHMEMX_P2P_SIGNAL=host, rccl_ar = RCCL's own ncclAllReduce "
-                               "with SHMEMX_RCCL_ALLREDUCE=2, the reference point: not SOS's "
-                               "order for fp sum, so not eligible for value then)")
+                               "SHMEMX_P2P_SIGNAL=host). rccl_ar = RCCL's own ncclAllReduce "
+                               "(SHMEMX_RCCL_ALLREDUCE=2) is reported as the reference point "
+                               "only: it measures RCCL's combine, not the library's fold")
     res["preflight"] = pre
     res["local_combine_all_pes"] = local_leg
     if curve:
@@ -337,23 +397,21 @@ def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed
     processes, each pinned to one host core, run the restated ring
     (oracle/sos_oracle.c oracle_pe_ring, src/collectives.c:647-764) over a /dev/shm
     segment -- memcpy puts and atomic pSync adds, SOS's XPMEM model -- on the same
-    per-PE inputs at the same nreduce.  Bounded sample: one untimed call, then as many
-    calls as fit ~6 s (max over ranks).  The CPU targets are compared byte for byte with
-    the library's ring result on the GPU for the same inputs.
+    per-PE inputs, at nreduce = 1Mi, 16Mi and the headline size (`rows`; the top-level
+    fields are the headline's).  Bounded sample per size: one untimed call, then as many
+    calls as fit ~6 s at the headline size (~1.5 s below it), max over ranks.  At each
+    size the CPU targets are compared byte for byte with the library's ring result on
+    the GPU for the same inputs.
     Test infrastructure in the timed-baseline role only: the product path never calls it."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if root not in sys.path:
         sys.path.insert(0, root)
     from oracle import oracle as O
     m = args.n
+    sizes = sorted({k for k in (1 << 20, 16 << 20) if k < m} | {m})
     opid = L.op_id(args.op)
     if rank == 0:
-        log(f"[cpu ring] {world} processes x 1 core, nreduce {m}")
-    # the library's ring on the GPU for these inputs (src holds fill(seed, rank) here)
-    S.shmemx_set_reduce_algorithm(L.ALGS["ring"])
-    fn(team, dst, src, m)
-    torch.cuda.synchronize()
-    S.shmemx_set_reduce_algorithm(L.ALGS[args.alg])
+        log(f"[cpu ring] {world} processes x 1 core, nreduce {sizes}")
 
     # one physical core per PE, consecutive (as a by-core rank binding would place them):
     # the first hardware thread of each core in the allowed set
@@ -368,7 +426,6 @@ def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed
         if first == c or first not in allowed:
             primaries.append(c)
     core = primaries[rank % len(primaries)]
-    os.sched_setaffinity(0, {core})
     path = f"/dev/shm/sosx_cpu_ring_{os.environ.get('MASTER_PORT', '0')}_{world}"
     ring = None
     why = ""
@@ -378,6 +435,7 @@ def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
         return v.item() == 0
 
+    rows = []
     try:
         ok = True
         if rank == 0:
@@ -400,25 +458,43 @@ def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed
             return {"skipped": why or "segment attach failed on a rank"}
         if rank == 0:
             os.unlink(path)  # every PE has it mapped
-        host_src = O.fill(dt, dist_kind, seed, rank, m)
-        t_warm = ring.time(opid, host_src, 1)
-        tw = torch.tensor([t_warm], dtype=torch.float64)
-        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
-        reps = max(1, min(10, int(6.0 / max(tw.item(), 1e-6))))
-        t = ring.time(opid, host_src, reps)
-        el = torch.tensor([t], dtype=torch.float64)
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        ts = el.item() / reps
-        ring.barrier()  # every put into this PE's target has landed
-        tgt = ring.target()
-        exp = torch.from_numpy(tgt.view("u1").copy()).to("cuda")
-        del tgt
-        torch.cuda.synchronize()
-        mm = L.count_mismatch(exp.data_ptr(), dst, m, es, stream)
-        mmt = torch.tensor([mm], dtype=torch.int64)
-        dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
-        del exp, host_src
-        ring.barrier()  # nobody unmaps before every PE has read its target
+        host_src = O.fill(dt, dist_kind, seed, rank, m)   # a prefix is the smaller sizes' input
+        for mk in sizes:
+            # the library's ring on the GPU for these inputs (src holds fill(seed, rank))
+            S.shmemx_set_reduce_algorithm(L.ALGS["ring"])
+            fn(team, dst, src, mk)
+            torch.cuda.synchronize()
+            S.shmemx_set_reduce_algorithm(L.ALGS[args.alg])
+            os.sched_setaffinity(0, {core})
+            ring.count = mk
+            t_warm = ring.time(opid, host_src, 1)
+            tw = torch.tensor([t_warm], dtype=torch.float64)
+            dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+            budget = 6.0 if mk == m else 1.5
+            reps = max(1, min(1000, int(budget / max(tw.item(), 1e-6))))
+            t = ring.time(opid, host_src, reps)
+            el = torch.tensor([t], dtype=torch.float64)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            ts = el.item() / reps
+            ring.barrier()  # every put into this PE's target has landed
+            os.sched_setaffinity(0, set(allowed))
+            tgt = ring.target()
+            exp = torch.from_numpy(tgt.view("u1").copy()).to("cuda")
+            del tgt
+            torch.cuda.synchronize()
+            mm = L.count_mismatch(exp.data_ptr(), dst, mk, es, stream)
+            mmt = torch.tensor([mm], dtype=torch.int64)
+            dist.all_reduce(mmt, op=dist.ReduceOp.SUM)
+            del exp
+            ring.barrier()  # nobody rewrites a target before every PE has read its own
+            rows.append({"nreduce": mk, "ms_per_call": round(ts * 1e3, 4),
+                         "value_GiBs": round(world * mk * es / ts / GiB, 3), "reps": reps,
+                         "bitwise_mismatches_vs_gpu_ring_all_ranks": int(mmt.item())})
+            if rank == 0:
+                log(f"[cpu ring] n={mk} {rows[-1]['ms_per_call']} ms/call, "
+                    f"{rows[-1]['value_GiBs']} GiB/s whole job, mismatches vs GPU ring "
+                    f"{rows[-1]['bitwise_mismatches_vs_gpu_ring_all_ranks']}")
+        del host_src
     finally:
         if ring is not None:
             ring.close()
@@ -429,17 +505,17 @@ def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed
             cpu = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
-    out = {"value": round(world * m * es / ts / GiB, 3), "unit": "GiB/s", "cores": world,
-           "kind": "port", "ms_per_call": round(ts * 1e3, 3),
+    head = rows[-1]
+    out = {"value": head["value_GiBs"], "unit": "GiB/s", "cores": world,
+           "kind": "port", "ms_per_call": round(head["ms_per_call"], 3),
            "sample": (f"SOS ring (oracle_pe_ring, src/collectives.c:647-764), "
                       f"shmem_{args.dtype}_{args.op}_reduce nreduce={m} per PE, {world} processes "
                       f"x 1 pinned physical core (consecutive cores from {primaries[0]}), "
-                      f"memcpy puts over /dev/shm, {reps} timed calls after 1 warm-up, gcc -O2; "
-                      f"host: {cpu}, {len(primaries)} cores / {len(allowed)} threads allowed"),
-           "bitwise_mismatches_vs_gpu_ring_all_ranks": int(mmt.item())}
-    if rank == 0:
-        log(f"[cpu ring] {out['ms_per_call']} ms/call, {out['value']} GiB/s whole job, "
-            f"mismatches vs GPU ring {out['bitwise_mismatches_vs_gpu_ring_all_ranks']}")
+                      f"memcpy puts over /dev/shm, {head['reps']} timed calls after 1 warm-up, "
+                      f"gcc -O2; host: {cpu}, {len(primaries)} cores / {len(allowed)} threads allowed"),
+           "bitwise_mismatches_vs_gpu_ring_all_ranks": sum(
+               r["bitwise_mismatches_vs_gpu_ring_all_ranks"] for r in rows),
+           "rows": rows}
     return out
 
 
@@ -744,7 +820,7 @@ def preflight(torch, dist, rank, world):
     why = ""
     import tempfile
     with tempfile.TemporaryFile("w+") as fo, tempfile.TemporaryFile("w+") as fe:
-        child = subprocess.Popen([sys.executable, "-u", "-m", "sos_amd.team_bench", "--preflight"],
+        child = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--preflight"],
                                  cwd=root, env=env, stdout=fo, stderr=fe)
         next_note = 20.0
         while child.poll() is None:
