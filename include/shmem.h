@@ -52,8 +52,11 @@
 #define SHMEM_THREAD_SERIALIZED 2
 #define SHMEM_THREAD_MULTIPLE   3
 
-/* teams (mpp/shmem-def.h.in) */
-typedef void *shmem_team_t;
+/* teams (mpp/shmem-def.h.in:94-96, :110): the same opaque handle type as SOS, so C++
+ * code that overloads or mangles on shmem_team_t links the same way */
+typedef struct shmem_impl_team_t {
+    int dummy;
+} * shmem_team_t;
 typedef struct {
     int num_contexts;
 } shmem_team_config_t;
@@ -65,7 +68,7 @@ extern "C" {
 
 extern shmem_team_t SHMEM_TEAM_WORLD;
 extern shmem_team_t SHMEM_TEAM_SHARED;
-#define SHMEM_TEAM_INVALID ((shmem_team_t) 0)
+#define SHMEM_TEAM_INVALID NULL
 
 /* ---- library setup, exit and query (src/init_c.c, src/query_c.c) ---------- */
 SHMEM_FUNCTION_ATTRIBUTES void shmem_init(void);

@@ -191,16 +191,10 @@ int sosx_set_rccl_allgather(int on);
  * value.  Collective switch; returns the previous mode, -1 if out of range. */
 int sosx_set_rccl_allreduce(int mode);
 
-/* Kernel variant selection for the hot fp32/generic combine (bench/tuning only):
- * returns the previous variant.  0 = default. */
-int sosx_set_combine_variant(int variant);
-int sosx_num_combine_variants(void);
-const char *sosx_combine_variant_name(int variant);
-/* Same for the 8-input fp32 sum fold: 0 = default (U=1), 1 = U=2, 2 = U=4. */
-int sosx_set_fold_variant(int variant);
-/* Same for the fp32 sum prefix (scans, 2..8 inputs): 0 = default, 1 = U=2, 2 = U=4,
- * 3 = U=1 plain loads/stores, 4 = U=2 plain, 5 = U=8 (U = 16-B vectors per lane). */
-int sosx_set_prefix_variant(int variant);
+/* The p2p transport's mapping flags (introspection for tests): the hipHostRegister
+ * flags of the shared pair-counter segment and the hipIpcOpenMemHandle flags of a peer's
+ * device heap. */
+void sosx_p2p_flags(unsigned *host_register, unsigned *ipc_open);
 
 /* Library / build identification. */
 const char *sosx_build_info(void);

@@ -77,9 +77,6 @@ _SIGS = {
     "sosx_memcpy": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p]),
     "sosx_combine_host": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_size_t,
                                      _c.c_size_t]),
-    "sosx_set_combine_variant": (_c.c_int, [_c.c_int]),
-    "sosx_num_combine_variants": (_c.c_int, []),
-    "sosx_combine_variant_name": (_c.c_char_p, [_c.c_int]),
     "sosx_build_info": (_c.c_char_p, []),
     "sosx_p2p_signal_mode": (_c.c_int, []),
     "sosx_set_p2p_signal_mode": (_c.c_int, [_c.c_int]),

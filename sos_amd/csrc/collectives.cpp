@@ -555,8 +555,13 @@ void op_to_all(void *target, const void *source, size_t count, size_t ts, const 
     if (rc) raise_error("%s: %s (datatype %d, op %d)", fn, status_text(rc), dt, op);
 
     int alg = sosplan::resolve_alg(s.reduce_alg, bytes, s.coll_size_crossover);
+    // the one-kernel forms fold at most SOSX_MAX_FOLD inputs: bigger teams keep the
+    // same element order through the pairwise schedules (ring/recdbl_direct: recdbl_sw
+    // tree by recursive halving; recdbl_gather: recdbl_sw itself)
     if ((alg == SOSX_ALG_RING || alg == SOSX_ALG_RECDBL_DIRECT) && t.size > SOSX_MAX_FOLD)
         alg = SOSX_ALG_RECHALVING;
+    if (alg == SOSX_ALG_RECDBL_GATHER && sosplan::pow2_floor(t.size) > SOSX_MAX_FOLD)
+        alg = SOSX_ALG_RECDBL;
     execute(alg, target, source, count, ts, t, op, dt, fn, true);
 }
 
@@ -576,6 +581,37 @@ void check_symmetric(const void *p, size_t bytes, const char *what, const char *
         raise_error("%s: argument \"%s\" (%p, %zu bytes) is not symmetric", fn, what, p, bytes);
 }
 
+// SHMEM_ERR_CHECK_ACTIVE_SET (src/shmem_internal.h:214-227) for the deprecated active-set
+// forms, whose stride is 1 << logPE_stride (src/collectives_c.c4:226).  SOS shifts
+// without a check (undefined for logPE_stride >= 31 or < 0) and tests the last member
+// with `> num_pes`; here both are refused: logPE_stride outside [0, 30], and a set whose
+// last member is not a PE.  The extent is computed in 64 bits (no int overflow).
+int active_set_stride(int PE_start, int logPE_stride, int PE_size, const char *fn)
+{
+    const State &s = st();
+    if (logPE_stride < 0 || logPE_stride > 30)
+        raise_error("%s: Invalid active set (PE_start = %d, logPE_stride = %d, PE_size = %d)", fn,
+                    PE_start, logPE_stride, PE_size);
+    const int stride = 1 << logPE_stride;
+    const long long last = (long long)PE_start + (long long)(PE_size - 1) * stride;
+    if (PE_start < 0 || PE_size < 0 || last >= s.n_pes)
+        raise_error("%s: Invalid active set (PE_start = %d, PE_stride = %d, PE_size = %d)", fn,
+                    PE_start, stride, PE_size);
+    if (!(s.my_pe >= PE_start && s.my_pe <= last && (s.my_pe - PE_start) % stride == 0))
+        raise_error("%s: Calling PE (%d) is not a member of the active set", fn, s.my_pe);
+    return stride;
+}
+
+// nelems * type_size for the size_t-count team forms: SOS multiplies unchecked; a count
+// whose byte size does not fit size_t is refused instead of wrapping.
+size_t checked_bytes(size_t nelems, size_t type_size, const char *what, const char *fn)
+{
+    if (type_size && nelems > SIZE_MAX / type_size)
+        raise_error("%s: Argument %s (%zu) times the element size (%zu) overflows size_t", fn, what,
+                    nelems, type_size);
+    return nelems * type_size;
+}
+
 }  // namespace
 
 extern "C" {
@@ -586,13 +622,7 @@ void sos_api_to_all(void *target, const void *source, int nreduce, size_t type_s
 {
     check_initialized(fn);
     State &s = st();
-    const int stride = 1 << logPE_stride;
-    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) >= s.n_pes)
-        raise_error("%s: Invalid active set (PE_start = %d, PE_stride = %d, PE_size = %d)", fn,
-                    PE_start, stride, PE_size);
-    if (!(s.my_pe >= PE_start && s.my_pe <= PE_start + ((PE_size - 1) * stride) &&
-          (s.my_pe - PE_start) % stride == 0))
-        raise_error("%s: Calling PE (%d) is not a member of the active set", fn, s.my_pe);
+    const int stride = active_set_stride(PE_start, logPE_stride, PE_size, fn);
     if (nreduce < 0)
         raise_error("%s: Argument nreduce must be greater or equal to zero (%ld)", fn, (long)nreduce);
     const size_t bytes = (size_t)nreduce * type_size;
@@ -620,7 +650,7 @@ int sos_api_reduce(shmem_team_t team, void *dest, const void *source, size_t nre
     check_initialized(fn);
     Team *t = team_from_handle(team);
     if (!t || !t->valid) raise_error("%s: invalid team", fn);
-    const size_t bytes = nreduce * type_size;
+    const size_t bytes = checked_bytes(nreduce, type_size, "nreduce", fn);
     check_symmetric(dest, bytes, "dest", fn);
     check_symmetric(source, bytes, "source", fn);
     check_overlap(dest, source, bytes, fn);
@@ -643,7 +673,7 @@ int sos_api_broadcast(shmem_team_t team, void *dest, const void *source, size_t 
     check_initialized(fn);
     Team *t = team_from_handle(team);
     if (!t || !t->valid) raise_error("%s: invalid team", fn);
-    const size_t bytes = nelems * type_size;
+    const size_t bytes = checked_bytes(nelems, type_size, "nelems", fn);
     check_symmetric(dest, bytes, "dest", fn);
     check_symmetric(source, bytes, "source", fn);
     check_overlap(dest, source, bytes, fn);
@@ -662,15 +692,9 @@ static void bcast_active_set(void *target, const void *source, size_t nlong, siz
 {
     check_initialized(fn);
     State &s = st();
-    const int stride = 1 << logPE_stride;
-    if (PE_start < 0 || stride < 1 || PE_size < 0 || PE_start + ((PE_size - 1) * stride) >= s.n_pes)
-        raise_error("%s: Invalid active set (PE_start = %d, PE_stride = %d, PE_size = %d)", fn,
-                    PE_start, stride, PE_size);
-    if (!(s.my_pe >= PE_start && s.my_pe <= PE_start + ((PE_size - 1) * stride) &&
-          (s.my_pe - PE_start) % stride == 0))
-        raise_error("%s: Calling PE (%d) is not a member of the active set", fn, s.my_pe);
+    const int stride = active_set_stride(PE_start, logPE_stride, PE_size, fn);
     check_root(PE_root, PE_size, fn);
-    const size_t bytes = nlong * ts;
+    const size_t bytes = checked_bytes(nlong, ts, "nlong", fn);
     check_symmetric(target, bytes, "target", fn);
     check_symmetric(source, bytes, "source", fn);
     check_symmetric(pSync, sizeof(long) * SHMEM_BCAST_SYNC_SIZE, "pSync", fn);
@@ -720,7 +744,7 @@ int sos_api_scan(shmem_team_t team, void *dest, const void *source, size_t nelem
     check_initialized(fn);
     Team *t = team_from_handle(team);
     if (!t || !t->valid) raise_error("%s: invalid team", fn);
-    const size_t bytes = nelems * type_size;
+    const size_t bytes = checked_bytes(nelems, type_size, "nelems", fn);
     check_symmetric(dest, bytes, "dest", fn);
     check_symmetric(source, bytes, "source", fn);
     check_overlap(dest, source, bytes, fn);

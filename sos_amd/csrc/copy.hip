@@ -39,17 +39,22 @@ template <int N> struct Sig {
     int nw, nq;
 };
 
+// A call whose earlier step already timed out (*err set) does not wait again: each later
+// step of the same call gives up at once, so a peer that died mid-call ends the call
+// after ONE timeout, not one per remaining step.  The error word is re-read inside the
+// spin too (another lane or workgroup of this step may have expired first).
 template <int N> __device__ __forceinline__ void sig_step(const Sig<N> &a, int i)
 {
     if (i < a.nw) __hip_atomic_store(a.waddr[i], a.wval[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();
-    if (i < a.nq) {
+    if (i < a.nq && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
         const long long t0 = wall_clock64();
         while (__hip_atomic_load(a.qaddr[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.qval[i]) {
             if (wall_clock64() - t0 > a.limit) {
                 __hip_atomic_store(a.err, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
+            if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
             __builtin_amdgcn_s_sleep(2);
         }
     }

@@ -9,146 +9,9 @@
 //   TREE  : the recdbl_sw butterfly (src/collectives.c:905-963).
 // P <= 8 (one PE per GPU on one node) is a template parameter; 9..64 run a runtime-P
 // element loop.
-#include "elementwise.h"
+#include "fold_kernels.h"
 
 namespace sos {
-
-// ---------------------------------------------------------------------------------
-// Fused P-way fold, P = NP known at compile time (one PE per GPU: P <= 8).
-// ---------------------------------------------------------------------------------
-struct FoldPtrs {
-    const void *p[SOSX_MAX_FOLD];
-};
-
-// recdbl_sw tree, evaluated from the perspective of the lowest PE of every subtree:
-// extras first (v[k] = v[k] OP v[k+pow2], src/collectives.c:920-926), then distance
-// 1, 2, 4, ... pairs (src/collectives.c:932-963).  Own value is always the left
-// operand, which makes the result bit-identical to recdbl_sw for commutative
-// element semantics (all integer ops, fp sum/prod without NaN payload choices).
-template <int NP> struct Pow2Floor {
-    static constexpr int v = NP >= 8 ? 8 : NP >= 4 ? 4 : NP >= 2 ? 2 : 1;
-};
-
-template <class T, class OP, int NP, int ORDER>
-__device__ __forceinline__ T fold_elem(const T (&v)[NP])
-{
-    if constexpr (ORDER == SOSX_ORDER_LINEAR) {
-        T acc = v[0];
-#pragma unroll
-        for (int k = 1; k < NP; ++k) acc = OP::f(acc, v[k]);
-        return acc;
-    } else {
-        constexpr int P2 = Pow2Floor<NP>::v;
-        T w[NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) w[k] = v[k];
-#pragma unroll
-        for (int k = 0; k < NP - P2; ++k) w[k] = OP::f(w[k], w[k + P2]);
-#pragma unroll
-        for (int d = 1; d < P2; d <<= 1)
-#pragma unroll
-            for (int k = 0; k < P2; k += 2 * d) w[k] = OP::f(w[k], w[k + d]);
-        return w[0];
-    }
-}
-
-template <class T, class OP, int NP, int ORDER>
-__device__ __forceinline__ u32x4 fold_pack(const u32x4 (&x)[NP])
-{
-    Pack<T> p[NP];
-#pragma unroll
-    for (int k = 0; k < NP; ++k) p[k] = __builtin_bit_cast(Pack<T>, x[k]);
-    Pack<T> r;
-#pragma unroll
-    for (int j = 0; j < Pack<T>::N; ++j) {
-        T v[NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) v[k] = p[k].e[j];
-        r.e[j] = fold_elem<T, OP, NP, ORDER>(v);
-    }
-    return __builtin_bit_cast(u32x4, r);
-}
-
-template <class T, class OP, int NP, int ORDER, int U>
-__global__ __launch_bounds__(kThreads) void k_fold(T *out, FoldPtrs ins, Geom g)
-{
-    constexpr int V = Pack<T>::N;
-    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
-    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
-        const size_t base = t * (size_t)(kThreads * U) + threadIdx.x;
-        u32x4 x[U][NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) {
-            const u32x4 *I = reinterpret_cast<const u32x4 *>((const T *)ins.p[k] + g.head);
-#pragma unroll
-            for (int u = 0; u < U; ++u) x[u][k] = ldv<true>(I + base + u * kThreads);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) stv<true>(O + base + u * kThreads, fold_pack<T, OP, NP, ORDER>(x[u]));
-    }
-    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
-        auto one = [&](size_t i) {
-            T v[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) v[k] = ((const T *)ins.p[k])[i];
-            out[i] = fold_elem<T, OP, NP, ORDER>(v);
-        };
-        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
-        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n;
-             i += kThreads)
-            one(i);
-    }
-}
-
-// Tuning variants of k_fold (bench A/B, sosx_set_fold_variant): each workgroup takes S
-// consecutive tiles (longer contiguous runs per input stream), optionally loading tile
-// j+1 before storing tile j (PF), optionally with an XCD-contiguous tile order
-// (workgroup w runs on XCD w % 8).  Same element order as k_fold.
-template <class T, class OP, int NP, int ORDER, int S, bool PF, bool XCD>
-__global__ __launch_bounds__(kThreads) void k_fold_st(T *out, FoldPtrs ins, Geom g, size_t groups)
-{
-    constexpr int V = Pack<T>::N;
-    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
-    size_t grp = blockIdx.x;
-    if (XCD && groups % 8 == 0 && grp < groups) grp = (grp % 8) * (groups / 8) + grp / 8;
-    if (grp < groups) {
-        const size_t t0 = grp * S;
-        const size_t t1 = t0 + S < g.tiles ? t0 + S : g.tiles;
-        u32x4 x[NP];
-        auto load = [&](size_t t, u32x4 (&d)[NP]) {
-            const size_t i = t * (size_t)kThreads + threadIdx.x;
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                d[k] = ldv<true>(reinterpret_cast<const u32x4 *>((const T *)ins.p[k] + g.head) + i);
-        };
-        if (PF) {
-            load(t0, x);
-            for (size_t t = t0; t < t1; ++t) {
-                u32x4 y[NP];
-                if (t + 1 < t1) load(t + 1, y);
-                stv<true>(O + t * (size_t)kThreads + threadIdx.x, fold_pack<T, OP, NP, ORDER>(x));
-#pragma unroll
-                for (int k = 0; k < NP; ++k) x[k] = y[k];
-            }
-        } else {
-            for (size_t t = t0; t < t1; ++t) {
-                load(t, x);
-                stv<true>(O + t * (size_t)kThreads + threadIdx.x, fold_pack<T, OP, NP, ORDER>(x));
-            }
-        }
-    }
-    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
-        auto one = [&](size_t i) {
-            T v[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) v[k] = ((const T *)ins.p[k])[i];
-            out[i] = fold_elem<T, OP, NP, ORDER>(v);
-        };
-        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
-        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
-            one(i);
-    }
-}
 
 template <class T, class OP, int NP, int ORDER>
 __global__ __launch_bounds__(kThreads) void k_fold_scalar(T *out, FoldPtrs ins,
@@ -206,62 +69,6 @@ __global__ __launch_bounds__(kThreads) void k_fold_dyn(T *out, FoldPtrs ins, int
 // runtime loop; the one input that may alias an output (`own`, the PE's own source
 // chunk under an in-place scan) is loaded before any store.
 // ---------------------------------------------------------------------------------
-constexpr int kMaxPrefix = 64;
-
-struct PrefixPtrs {
-    const void *in[kMaxPrefix];
-    void *out[kMaxPrefix];
-};
-
-// 16-B vectors per lane per tile.  U = 2/4/8 and plain loads/stores measured slower over
-// random buffer layouts (profiles/r2_prefix_variants*.txt); they stay as
-// bench variants (sosx_set_prefix_variant).
-constexpr int kPrefixU = 1;
-
-// NT: nontemporal loads/stores (the default); the plain variant is a bench A/B only.
-template <class T, class OP, int NP, int U, bool NT = true>
-__global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
-{
-    constexpr int V = Pack<T>::N;
-    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
-        const size_t base = t * (size_t)(kThreads * U) + threadIdx.x;
-        u32x4 x[U][NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k)
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                x[u][k] = ldv<NT>(reinterpret_cast<const u32x4 *>((const T *)p.in[k] + g.head) + base + u * kThreads);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const size_t i = base + u * kThreads;
-            u32x4 acc = x[u][0];
-            stv<NT>(reinterpret_cast<u32x4 *>((T *)p.out[0] + g.head) + i, acc);
-#pragma unroll
-            for (int k = 1; k < NP; ++k) {
-                acc = apply<T, OP>(acc, x[u][k]);
-                stv<NT>(reinterpret_cast<u32x4 *>((T *)p.out[k] + g.head) + i, acc);
-            }
-        }
-    }
-    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
-        auto one = [&](size_t i) {
-            T v[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) v[k] = ((const T *)p.in[k])[i];
-            T acc = v[0];
-            ((T *)p.out[0])[i] = acc;
-#pragma unroll
-            for (int k = 1; k < NP; ++k) {
-                acc = OP::f(acc, v[k]);
-                ((T *)p.out[k])[i] = acc;
-            }
-        };
-        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
-        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n; i += kThreads)
-            one(i);
-    }
-}
-
 template <class T, class OP>
 __device__ __forceinline__ void prefix_elem_dyn(const PrefixPtrs &p, int np, int own, size_t i)
 {
@@ -289,30 +96,6 @@ using namespace sos;
 
 namespace {
 
-int g_fold_variant = 0;  // tuning experiments on the 8-input fp32 sum fold (bench A/B)
-int g_prefix_variant = 0;  // same for the fp32 sum prefix, 2..8 inputs
-
-template <class T, class OP, int NP, int ORDER, int U>
-int launch_fold_u(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
-{
-    Geom g = make_geom((uintptr_t)out, n, sizeof(T), U);
-    hipLaunchKernelGGL((k_fold<T, OP, NP, ORDER, U>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
-                       0, st, out, ins, g);
-    return hip_ok(hipGetLastError());
-}
-
-template <class T, class OP, int NP, int ORDER, int S, bool PF, bool XCD>
-int launch_fold_st(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
-{
-    Geom g = make_geom((uintptr_t)out, n, sizeof(T), 1);
-    const size_t groups = (g.tiles + S - 1) / S;
-    unsigned blocks = (unsigned)(groups + (g.has_rem ? 1 : 0));
-    if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL((k_fold_st<T, OP, NP, ORDER, S, PF, XCD>), dim3(blocks), dim3(kThreads), 0, st,
-                       out, ins, g, groups);
-    return hip_ok(hipGetLastError());
-}
-
 template <class T, class OP, int NP, int ORDER>
 int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 {
@@ -325,16 +108,6 @@ int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
         hipLaunchKernelGGL((k_fold_scalar<T, OP, NP, ORDER>), dim3((unsigned)blocks),
                            dim3(kThreads), 0, st, out, ins, n);
         return hip_ok(hipGetLastError());
-    }
-    if constexpr (std::is_same<T, float>::value && std::is_same<OP, OpSum>::value && NP == 8 &&
-                  ORDER == SOSX_ORDER_LINEAR) {
-        if (g_fold_variant == 1) return launch_fold_u<T, OP, NP, ORDER, 2>(out, ins, n, st);
-        if (g_fold_variant == 2) return launch_fold_u<T, OP, NP, ORDER, 4>(out, ins, n, st);
-        if (g_fold_variant == 3) return launch_fold_st<T, OP, NP, ORDER, 4, false, false>(out, ins, n, st);
-        if (g_fold_variant == 4) return launch_fold_st<T, OP, NP, ORDER, 16, false, false>(out, ins, n, st);
-        if (g_fold_variant == 5) return launch_fold_st<T, OP, NP, ORDER, 1, false, true>(out, ins, n, st);
-        if (g_fold_variant == 6) return launch_fold_st<T, OP, NP, ORDER, 4, true, false>(out, ins, n, st);
-        if (g_fold_variant == 7) return launch_fold_st<T, OP, NP, ORDER, 16, true, true>(out, ins, n, st);
     }
     constexpr int U = NP <= 2 ? 4 : (NP <= 4 ? 2 : 1);
     Geom g = make_geom(o, n, sizeof(T), U);
@@ -373,25 +146,13 @@ struct FoldFn {
     }
 };
 
-template <class T, class OP, int NP, int U, bool NT>
-int launch_prefix_u(const PrefixPtrs &p, size_t n, hipStream_t st)
-{
-    Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), U);
-    hipLaunchKernelGGL((k_prefix<T, OP, NP, U, NT>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st, p, g);
-    return hip_ok(hipGetLastError());
-}
-
 template <class T, class OP, int NP>
 int launch_prefix_np(const PrefixPtrs &p, size_t n, hipStream_t st)
 {
-    if constexpr (std::is_same<T, float>::value && std::is_same<OP, OpSum>::value && NP >= 2) {
-        if (g_prefix_variant == 1) return launch_prefix_u<T, OP, NP, 2, true>(p, n, st);
-        if (g_prefix_variant == 2) return launch_prefix_u<T, OP, NP, 4, true>(p, n, st);
-        if (g_prefix_variant == 3) return launch_prefix_u<T, OP, NP, 1, false>(p, n, st);
-        if (g_prefix_variant == 4) return launch_prefix_u<T, OP, NP, 2, false>(p, n, st);
-        if (g_prefix_variant == 5) return launch_prefix_u<T, OP, NP, 8, true>(p, n, st);
-    }
-    return launch_prefix_u<T, OP, NP, kPrefixU, true>(p, n, st);
+    Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), kPrefixU);
+    hipLaunchKernelGGL((k_prefix<T, OP, NP, kPrefixU, true>), dim3(grid_for(g, kNoCap)),
+                       dim3(kThreads), 0, st, p, g);
+    return hip_ok(hipGetLastError());
 }
 
 struct PrefixFn {
@@ -445,26 +206,6 @@ int sosx_prefix(int op, int dtype, void *const *outs, const void *const *ins, in
         pp.out[k] = outs[k];
     }
     return dispatch<PrefixFn>(op, dtype, &pp, np, own, count, as_stream(stream));
-}
-
-// Tuning knob (bench A/B only) for the 8-input fp32 sum LINEAR fold: 0 = default,
-// 1 = U=2, 2 = U=4, 3/4 = 4/16 consecutive tiles per workgroup, 5 = XCD-contiguous
-// tile order, 6 = 4 tiles with the next tile's loads issued before the store,
-// 7 = 16 tiles prefetched, XCD-contiguous.  Returns the previous value.
-int sosx_set_fold_variant(int v)
-{
-    const int prev = g_fold_variant;
-    if (v >= 0 && v <= 7) g_fold_variant = v;
-    return prev;
-}
-
-// Same for the 8-input fp32 sum prefix: 0 = default (U=1, nontemporal), 1 = U=2,
-// 2 = U=4, 3 = U=1 plain loads/stores, 4 = U=2 plain, 5 = U=8.  Returns the previous value.
-int sosx_set_prefix_variant(int v)
-{
-    const int prev = g_prefix_variant;
-    if (v >= 0 && v <= 5) g_prefix_variant = v;
-    return prev;
 }
 
 int sosx_fold(int op, int dtype, int order, void *out, const void *const *ins, int nin,

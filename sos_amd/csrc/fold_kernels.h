@@ -1,0 +1,152 @@
+// fold_kernels.h -- the fused P-way fold (k_fold) and the fused prefix (k_prefix), the
+// team schedules' local steps, shared by the product library (fold.hip) and the
+// bench-only variant library (tools/variants/variants.hip).
+#pragma once
+#include "elementwise.h"
+
+namespace sos {
+
+// ---------------------------------------------------------------------------------
+// Fused P-way fold, P = NP known at compile time (one PE per GPU: P <= 8).
+// ---------------------------------------------------------------------------------
+struct FoldPtrs {
+    const void *p[SOSX_MAX_FOLD];
+};
+
+// recdbl_sw tree, evaluated from the perspective of the lowest PE of every subtree:
+// extras first (v[k] = v[k] OP v[k+pow2], src/collectives.c:920-926), then distance
+// 1, 2, 4, ... pairs (src/collectives.c:932-963).  Own value is always the left
+// operand, which makes the result bit-identical to recdbl_sw for commutative
+// element semantics (all integer ops, fp sum/prod without NaN payload choices).
+template <int NP> struct Pow2Floor {
+    static constexpr int v = NP >= 8 ? 8 : NP >= 4 ? 4 : NP >= 2 ? 2 : 1;
+};
+
+template <class T, class OP, int NP, int ORDER>
+__device__ __forceinline__ T fold_elem(const T (&v)[NP])
+{
+    if constexpr (ORDER == SOSX_ORDER_LINEAR) {
+        T acc = v[0];
+#pragma unroll
+        for (int k = 1; k < NP; ++k) acc = OP::f(acc, v[k]);
+        return acc;
+    } else {
+        constexpr int P2 = Pow2Floor<NP>::v;
+        T w[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) w[k] = v[k];
+#pragma unroll
+        for (int k = 0; k < NP - P2; ++k) w[k] = OP::f(w[k], w[k + P2]);
+#pragma unroll
+        for (int d = 1; d < P2; d <<= 1)
+#pragma unroll
+            for (int k = 0; k < P2; k += 2 * d) w[k] = OP::f(w[k], w[k + d]);
+        return w[0];
+    }
+}
+
+template <class T, class OP, int NP, int ORDER>
+__device__ __forceinline__ u32x4 fold_pack(const u32x4 (&x)[NP])
+{
+    Pack<T> p[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) p[k] = __builtin_bit_cast(Pack<T>, x[k]);
+    Pack<T> r;
+#pragma unroll
+    for (int j = 0; j < Pack<T>::N; ++j) {
+        T v[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) v[k] = p[k].e[j];
+        r.e[j] = fold_elem<T, OP, NP, ORDER>(v);
+    }
+    return __builtin_bit_cast(u32x4, r);
+}
+
+template <class T, class OP, int NP, int ORDER, int U>
+__global__ __launch_bounds__(kThreads) void k_fold(T *out, FoldPtrs ins, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t base = t * (size_t)(kThreads * U) + threadIdx.x;
+        u32x4 x[U][NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const u32x4 *I = reinterpret_cast<const u32x4 *>((const T *)ins.p[k] + g.head);
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u][k] = ldv<true>(I + base + u * kThreads);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) stv<true>(O + base + u * kThreads, fold_pack<T, OP, NP, ORDER>(x[u]));
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)ins.p[k])[i];
+            out[i] = fold_elem<T, OP, NP, ORDER>(v);
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n;
+             i += kThreads)
+            one(i);
+    }
+}
+
+constexpr int kMaxPrefix = 64;
+
+struct PrefixPtrs {
+    const void *in[kMaxPrefix];
+    void *out[kMaxPrefix];
+};
+
+// 16-B vectors per lane per tile.  U = 2/4/8 and plain loads/stores measured slower over
+// random buffer layouts (profiles/r2_prefix_variants*.txt); they are kept in
+// the bench-only variant library (tools/variants/).
+constexpr int kPrefixU = 1;
+
+// NT: nontemporal loads/stores (the default); plain loads/stores are a bench A/B only.
+template <class T, class OP, int NP, int U, bool NT = true>
+__global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t base = t * (size_t)(kThreads * U) + threadIdx.x;
+        u32x4 x[U][NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                x[u][k] = ldv<NT>(reinterpret_cast<const u32x4 *>((const T *)p.in[k] + g.head) + base + u * kThreads);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + u * kThreads;
+            u32x4 acc = x[u][0];
+            stv<NT>(reinterpret_cast<u32x4 *>((T *)p.out[0] + g.head) + i, acc);
+#pragma unroll
+            for (int k = 1; k < NP; ++k) {
+                acc = apply<T, OP>(acc, x[u][k]);
+                stv<NT>(reinterpret_cast<u32x4 *>((T *)p.out[k] + g.head) + i, acc);
+            }
+        }
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)p.in[k])[i];
+            T acc = v[0];
+            ((T *)p.out[0])[i] = acc;
+#pragma unroll
+            for (int k = 1; k < NP; ++k) {
+                acc = OP::f(acc, v[k]);
+                ((T *)p.out[k])[i] = acc;
+            }
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
+}  // namespace sos

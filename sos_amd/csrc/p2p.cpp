@@ -35,6 +35,7 @@
 //   host (SHMEMX_P2P_SIGNAL=host, or when HIP cannot register the segment): the host
 //     synchronises the stream and moves the counters itself every round, as steps 1-4.
 #include <time.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -122,6 +123,23 @@ template <class X> X *dev(X *host)
 
 // Wall-clock bound of one wait (SHMEMX_P2P_TIMEOUT seconds, default 300): a peer that
 // never posts ends the job with a message instead of hanging it.
+// Test hook (tests/test_gpu_multipe.py::test_p2p_stall_mid_call): the PE named by
+// SOSX_P2P_TEST_STALL_PE stops for 60 s right after the entry boundary of its first
+// multi-round call, so its peers meet the bounded DEVICE waits of the later rounds.
+void stall_hook()
+{
+    static const int pe = [] {
+        const char *e = getenv("SOSX_P2P_TEST_STALL_PE");
+        return e && *e ? atoi(e) : -1;
+    }();
+    static bool done = false;
+    if (pe == st().my_pe && !done) {
+        done = true;
+        fprintf(stderr, "[%04d] test hook: stalling 60 s after the call's entry boundary\n", pe);
+        sleep(60);
+    }
+}
+
 double wait_limit_s()
 {
     static const double lim = [] {
@@ -413,6 +431,7 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
             for (const auto &x : r.xfers) sends |= x.send != 0;
             if (sends && hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
             host_flush();
+            stall_hook();
         } else {
             step_pending = true;
         }
@@ -532,9 +551,10 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
 
 // Signalling setup (runtime.cpp ensure_device_heap, collective): register the shared
 // segment with HIP on every PE and agree through the bootstrap whether stream mode is
-// possible everywhere.  The mode in use starts as SHMEMX_P2P_SIGNAL (stream by default
-// when every PE can: equal or faster than host mode in every one-GPU measurement,
-// profiles/r2_p2p_signal_latency.txt) and can be switched collectively
+// possible everywhere.  The mode in use starts as SHMEMX_P2P_SIGNAL; unset, it is stream
+// when every PE drives the same GPU (equal or faster than host mode in every one-GPU
+// measurement, profiles/r2_p2p_signal_latency.txt) and host when the PEs span several
+// GPUs (stream mode across xGMI is unmeasured).  It can be switched collectively
 // (sosx_set_p2p_signal_mode).
 void p2p_signal_setup()
 {
@@ -549,7 +569,7 @@ void p2p_signal_setup()
     void *dptr = nullptr;
     if (!g_sig.registered) {
         const size_t bytes = (sizeof(P2PShared) + 4095) & ~(size_t)4095;
-        hipError_t he = hipHostRegister(s.shm.extra, bytes, hipHostRegisterMapped);
+        hipError_t he = hipHostRegister(s.shm.extra, bytes, kP2PHostRegisterFlags);
         if (he == hipSuccess) g_sig.registered = true;
         else {
             (void)hipGetLastError();
@@ -568,17 +588,36 @@ void p2p_signal_setup()
         (void)hipGetLastError();
         ok = 0;
     }
-    std::vector<int> oks((size_t)s.n_pes);
-    if (sosboot::hub_allgather(&s.hub, &ok, sizeof(ok), oks.data()) != 0)
+    // which GPU this PE drives (PCI bus id): stream mode is the default only when every
+    // PE shares one device -- the configuration every stream-mode measurement and test
+    // ran in.  Across GPUs the device-side flags cross xGMI through host memory, which
+    // no run has covered yet, so the default there is host signalling.
+    struct Vote { int ok; char bus[20]; } mine, *votes;
+    memset(&mine, 0, sizeof(mine));
+    mine.ok = ok;
+    if (hipDeviceGetPCIBusId(mine.bus, (int)sizeof(mine.bus) - 1, s.device) != hipSuccess) {
+        (void)hipGetLastError();
+        snprintf(mine.bus, sizeof(mine.bus), "dev%d", s.device);
+    }
+    std::vector<Vote> all((size_t)s.n_pes);
+    votes = all.data();
+    if (sosboot::hub_allgather(&s.hub, &mine, sizeof(mine), votes) != 0)
         raise_error("p2p: signalling mode agreement failed");
-    for (int v : oks) ok &= v;
+    bool one_device = true;
+    for (const Vote &v : all) {
+        ok &= v.ok;
+        one_device &= strncmp(v.bus, all[0].bus, sizeof(v.bus)) == 0;
+    }
     g_sig.capable = ok != 0;
     g_sig.dbase = (char *)dptr;
     g_sig.limit_ticks = (long long)(wait_limit_s() * 1e3 * (double)rate_khz);
-    const char *e = getenv("SHMEMX_P2P_SIGNAL");  // the same on every PE (job environment)
-    g_sig.on = g_sig.capable && !(e && strcmp(e, "host") == 0);
-    debug_msg("p2p transport signalling: %s (stream mode %s)", g_sig.on ? "stream" : "host",
-              g_sig.capable ? "available" : "unavailable");
+    // SHMEMX_P2P_SIGNAL = stream | host (the same on every PE: job environment); unset:
+    // stream on one device, host across devices
+    const char *e = getenv("SHMEMX_P2P_SIGNAL");
+    const bool want = e && *e ? strcmp(e, "host") != 0 : one_device;
+    g_sig.on = g_sig.capable && want;
+    debug_msg("p2p transport signalling: %s (stream mode %s; PEs on %s)", g_sig.on ? "stream" : "host",
+              g_sig.capable ? "available" : "unavailable", one_device ? "one device" : "several devices");
 }
 
 void p2p_signal_teardown()

@@ -38,14 +38,6 @@ Local fold2(int out_buf, uint64_t out_off, int a_buf, uint64_t a_off, int b_buf,
     return l;
 }
 
-// Largest power of two <= P (src/collectives.c:878-882 for P >= 2).
-int pow2_floor(int P)
-{
-    int p = 1;
-    while (p * 2 <= P) p *= 2;
-    return p;
-}
-
 // RING and RECDBL_DIRECT share the data movement: a direct reduce-scatter of the SOS
 // ring chunks (chunk c is owned, folded and broadcast by team index c), then a
 // direct allgather.  Only the fold order differs.
@@ -435,6 +427,14 @@ int build_bcast(int root, bool copy_root, int P, int me, uint64_t count, uint64_
 }
 
 }  // namespace
+
+// Largest power of two <= P (src/collectives.c:878-882 for P >= 2).
+int pow2_floor(int P)
+{
+    int p = 1;
+    while (p * 2 <= P) p *= 2;
+    return p;
+}
 
 void ring_chunk(uint64_t count, int P, int c, uint64_t *n, uint64_t *first)
 {

@@ -53,7 +53,7 @@ enum Kind : int { FOLD = 0, COPY = 1, PREFIX = 2, ZERO = 3 };
 constexpr int PLAN_INSCAN = 16;
 constexpr int PLAN_EXSCAN = 17;
 constexpr int PLAN_BCAST = 32;
-constexpr int PLAN_MAX_PE = 64;   // scans/broadcast (the direct reductions stop at 8)
+constexpr int PLAN_MAX_PE = 64;   // inputs of one local op: SOSX_MAX_FOLD folds, scan prefixes
 inline bool is_scan(int alg) { return alg == PLAN_INSCAN || alg == PLAN_EXSCAN; }
 inline bool is_bcast(int alg) { return alg >= PLAN_BCAST; }
 inline int bcast_alg(int root, bool copy_root) { return PLAN_BCAST + 2 * root + (copy_root ? 1 : 0); }
@@ -94,6 +94,9 @@ struct Plan {
     bool writes_dst = true;    // false: a broadcast root without copy leaves its target
     bool scr_sent = false;     // true: some transfer sends out of SCR (scans)
 };
+
+// Largest power of two <= P (src/collectives.c:878-882).
+int pow2_floor(int P);
 
 // SOS ring chunk c of `count` elements over P PEs (src/collectives.c:697-709).
 void ring_chunk(uint64_t count, int P, int c, uint64_t *n, uint64_t *first);

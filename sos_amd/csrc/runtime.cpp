@@ -286,20 +286,34 @@ void ensure_device_heap()
              s.dev_heap_bytes, rtv);
         return;
     }
-    hipIpcMemHandle_t mine;
+    struct Export { hipIpcMemHandle_t h; int device; } mine;
     memset(&mine, 0, sizeof(mine));
-    hipError_t e = hipIpcGetMemHandle(&mine, base);
+    mine.device = s.device;
+    hipError_t e = hipIpcGetMemHandle(&mine.h, base);
     if (e != hipSuccess && fatal) hip_check(e, "hipIpcGetMemHandle(device heap)");
     debug_msg("device heap: IPC handle %s", e == hipSuccess ? "ok" : hipGetErrorString(e));
-    std::vector<hipIpcMemHandle_t> all((size_t)s.n_pes);
+    std::vector<Export> all((size_t)s.n_pes);
     if (sosboot::hub_allgather(&s.hub, &mine, sizeof(mine), all.data()) != 0)
         raise_error("device heap: IPC handle exchange failed");
     int ok = e == hipSuccess;
     for (int q = 0; q < s.n_pes && ok; ++q) {
         if (q == s.my_pe) continue;
+        // a heap on another GPU (device ordinals are node-global: one process per GPU,
+        // no HIP_VISIBLE_DEVICES remapping) is read in place only with peer access
+        const int pd = all[(size_t)q].device;
+        int can = 1;
+        if (pd != s.device && (hipDeviceCanAccessPeer(&can, s.device, pd) != hipSuccess || !can)) {
+            (void)hipGetLastError();
+            if (fatal)
+                raise_error("p2p transport: GPU %d cannot access PE %d's GPU %d (hipDeviceCanAccessPeer)",
+                            s.device, q, pd);
+            warn("GPU %d cannot access PE %d's GPU %d: p2p transport off", s.device, q, pd);
+            ok = 0;
+            break;
+        }
         void *p = nullptr;
-        debug_msg("device heap: opening PE %d's handle", q);
-        hipError_t eo = hipIpcOpenMemHandle(&p, all[(size_t)q], hipIpcMemLazyEnablePeerAccess);
+        debug_msg("device heap: opening PE %d's handle (GPU %d)", q, pd);
+        hipError_t eo = hipIpcOpenMemHandle(&p, all[(size_t)q].h, kP2PIpcOpenFlags);
         debug_msg("device heap: PE %d mapped at %p (%s)", q, p, hipGetErrorString(eo));
         if (eo != hipSuccess) {
             if (fatal) hip_check(eo, "hipIpcOpenMemHandle(peer device heap)");
@@ -405,7 +419,7 @@ void team_barrier(const Team &t)
     hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize(barrier)");
 }
 
-Team *team_from_handle(void *handle) { return (Team *)handle; }
+Team *team_from_handle(shmem_team_t handle) { return reinterpret_cast<Team *>(handle); }
 
 // ---------------------------------------------------------------------------------
 // init (src/init.c:221-567, condensed to what the reduction path needs)
@@ -462,9 +476,9 @@ static void init_common(int pe, int npes, const ncclUniqueId *uid)
     s.shared.psync_idx = 1;
     s.node = s.world;    // SHMEMX_TEAM_NODE (:101-164)
     s.node.psync_idx = 2;
-    SHMEM_TEAM_WORLD = &s.world;
-    SHMEM_TEAM_SHARED = &s.shared;
-    SHMEMX_TEAM_NODE = &s.node;
+    SHMEM_TEAM_WORLD = team_handle(&s.world);
+    SHMEM_TEAM_SHARED = team_handle(&s.shared);
+    SHMEMX_TEAM_NODE = team_handle(&s.node);
     // team slots (src/shmem_team.c:171-226): 64 at most, 3 at least, 0..2 predefined
     if (s.teams_max > 64) raise_error("Requested %ld teams, but only 64 are supported", s.teams_max);
     if (s.teams_max < 3) s.teams_max = 3;
@@ -1089,7 +1103,7 @@ int shmem_team_split_strided(shmem_team_t parent_team, int PE_start, int PE_stri
             s.team_avail &= ~(1ull << slot);
             Team *t = new Team(child);
             s.team_pool[(size_t)slot] = t;
-            if (new_team) *new_team = t;
+            if (new_team) *new_team = team_handle(t);
         }
     }
     team_barrier(*parent);  // src/shmem_team.c:410-414
@@ -1143,7 +1157,7 @@ void shmem_team_destroy(shmem_team_t team)
     // src/teams_c.c4:138-148, src/shmem_team.c:508-535
     check_initialized("shmem_team_destroy");
     State &s = st();
-    if (team == &s.world || team == &s.shared)
+    if (team == team_handle(&s.world) || team == team_handle(&s.shared))
         raise_error("Cannot destroy a pre-defined team");
     Team *t = team_from_handle(team);
     if (!t || t->predefined) return;
@@ -1163,3 +1177,10 @@ int shmem_team_sync(shmem_team_t team)
 }
 
 }  // extern "C"
+
+// Introspection for the CPU tests (tests/test_abi.py): the p2p transport's mapping flags.
+extern "C" void sosx_p2p_flags(unsigned *host_register, unsigned *ipc_open)
+{
+    if (host_register) *host_register = sosrt::kP2PHostRegisterFlags;
+    if (ipc_open) *ipc_open = sosrt::kP2PIpcOpenFlags;
+}

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "bootstrap.h"
+#include "shmem.h"
 #include "sosx.h"
 
 namespace sosrt {
@@ -152,7 +153,22 @@ bool is_symmetric(const void *p, size_t bytes);
 // Barrier across a team: dissemination over RCCL point-to-point, host-synchronous.
 void team_barrier(const Team &t);
 
-Team *team_from_handle(void *handle);
+// shmem_team_t is SOS's opaque `struct shmem_impl_team_t *` (mpp/shmem-def.h.in:94-96);
+// the object behind it is a Team.
+// Flags of the p2p transport's two cross-process mappings:
+//  * the node shared segment of pair counters is registered with hipHostRegister:
+//    Mapped (a device pointer through hipHostGetDevicePointer on the PE's own GPU) and
+//    NOT hipExtHostRegisterCoarseGrained, so it is fine-grained system memory, coherent
+//    for the device's system-scope atomic loads/stores (the device only loads and
+//    stores these words, no read-modify-write, so no PCIe AtomicOp support is needed);
+//  * a peer's device heap is opened with hipIpcOpenMemHandle(hipIpcMemLazyEnablePeerAccess),
+//    which enables peer access from this PE's GPU to the exporter's GPU (required when
+//    they differ; hipDeviceCanAccessPeer is checked first).
+constexpr unsigned kP2PHostRegisterFlags = hipHostRegisterMapped;
+constexpr unsigned kP2PIpcOpenFlags = hipIpcMemLazyEnablePeerAccess;
+
+Team *team_from_handle(shmem_team_t handle);
+inline shmem_team_t team_handle(Team *t) { return reinterpret_cast<shmem_team_t>(t); }
 
 // The device symmetric heap (created collectively; IPC-exported to every PE when the
 // peer-to-peer transport is on).

@@ -156,3 +156,56 @@ def test_one_hip_runtime_per_process(order):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "one runtime" in r.stdout
+
+
+def test_team_handle_is_sos_type(tmp_path):
+    """shmem_team_t is SOS's `struct shmem_impl_team_t *` (mpp/shmem-def.h.in:94-96) and
+    SHMEM_TEAM_INVALID is NULL (:110): a C++ library built against SOS's typedef (the
+    first TU below restates it, as code compiled against SOS's shmem.h sees it), with a
+    function overloaded on the handle type, links with user code built against this
+    include/shmem.h -- the mangled names agree -- and C rejects a pointer of another type."""
+    lib_tu = tmp_path / "sos_side.cpp"
+    lib_tu.write_text(
+        "typedef struct shmem_impl_team_t { int dummy; } * shmem_team_t;\n"
+        "int team_tag(shmem_team_t t) { return t ? 1 : 2; }\n"
+        "int team_tag(void *p) { return p ? 3 : 4; }\n")
+    user_tu = tmp_path / "user.cpp"
+    user_tu.write_text(
+        "#include <shmem.h>\n#include <stdio.h>\n"
+        "int team_tag(shmem_team_t t);\nint team_tag(void *p);\n"
+        "int main(void){ shmem_team_t t = SHMEM_TEAM_INVALID; int x = 0;\n"
+        "  printf(\"%d %d %d\\n\", team_tag(t), team_tag((void *)&x), t == NULL); return 0; }\n")
+    exe = str(tmp_path / "a.out")
+    r = subprocess.run(["g++", "-std=c++17", "-Wall", "-I", INC, str(lib_tu), str(user_tu), "-o", exe],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    assert out == ["2", "3", "1"], out
+    bad = tmp_path / "bad.c"
+    bad.write_text("#include <shmem.h>\nint main(void){ int x; shmem_team_t t = &x; return t != 0; }\n")
+    r = subprocess.run(["gcc", "-std=gnu11", "-Werror=incompatible-pointer-types", "-I", INC,
+                        "-c", str(bad), "-o", str(tmp_path / "bad.o")], capture_output=True, text=True)
+    assert r.returncode != 0 and "incompatible" in r.stderr, r.stderr
+
+
+def _hip_define(name):
+    text = open("/opt/rocm/include/hip/hip_runtime_api.h").read()
+    m = re.search(rf"#define {name} (0x[0-9a-fA-F]+|\d+)", text)
+    assert m, name
+    return int(m.group(1), 0)
+
+
+def test_p2p_mapping_flags():
+    """The p2p transport's cross-process mappings, against the HIP
+    headers: the pair-counter segment is hipHostRegister'ed Mapped and fine-grained (not
+    hipExtHostRegisterCoarseGrained, not the uncached/IO variants), and a peer's heap is
+    opened with hipIpcMemLazyEnablePeerAccess (peer access to another GPU)."""
+    import ctypes
+    from sos_amd import _lib
+    L = _lib.lib()
+    reg, ipc = ctypes.c_uint(0xFFFF), ctypes.c_uint(0xFFFF)
+    L.sosx_p2p_flags(ctypes.byref(reg), ctypes.byref(ipc))
+    assert reg.value & _hip_define("hipHostRegisterMapped")
+    for bad in ("hipExtHostRegisterCoarseGrained", "hipHostRegisterIoMemory", "hipExtHostRegisterUncached"):
+        assert not reg.value & _hip_define(bad), bad
+    assert ipc.value == _hip_define("hipIpcMemLazyEnablePeerAccess")

@@ -88,27 +88,6 @@ def test_prefix_kernel_aliasing(torch_cuda, np_):
         assert np.array_equal(bits(from_dev(do[k], ref[k])), bits(ref[k])), (np_, k)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
-def test_prefix_kernel_variants(torch_cuda, variant):
-    """The bench A/B shapes of the 8-input fp32 sum prefix (sosx_set_prefix_variant):
-    U = 2 / 4 vectors per lane, plain loads/stores.  Ragged head and tail included."""
-    torch = torch_cuda
-    lib = _lib.lib()
-    dt, n, pad = 23, (1 << 18) + 1029, 4
-    ins = [src_of(dt, 77, k, n) for k in range(8)]
-    ref = cpu_prefix(5, dt, ins)
-    di = [to_dev(torch, a, pad) for a in ins]
-    do = [torch.zeros_like(t) for t in di]
-    prev = lib.sosx_set_prefix_variant(variant)
-    try:
-        _lib.prefix(5, dt, [t.data_ptr() + pad for t in do], [t.data_ptr() + pad for t in di], n)
-        torch.cuda.synchronize()
-    finally:
-        lib.sosx_set_prefix_variant(prev)
-    for k in range(8):
-        assert np.array_equal(bits(from_dev(do[k], ref[k], pad)), bits(ref[k])), (variant, k)
-
-
 @pytest.mark.parametrize("P", [9, 12, 16, 64])
 @pytest.mark.parametrize("order", [0, 1])
 @pytest.mark.parametrize("dt,op", [(23, 5), (11, 2), (27, 6), (4, 4)])

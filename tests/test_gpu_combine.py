@@ -293,27 +293,6 @@ def test_combine_host_pipeline(torch_cuda, sos, oracle, dt, op):
         assert check(dt, op, got, ref), (dt, op, n, chunk)
 
 
-def test_every_combine_variant_bit_exact(torch_cuda, sos, oracle):
-    """The tuning variants (bench.py --variants) compute the same fp32 sum as the default."""
-    torch = torch_cuda
-    L = sos.lib()
-    n = (1 << 22) + 4099
-    a, b = oracle.fill(23, 0, 77, 0, n), oracle.fill(23, 0, 77, 1, n)
-    ref = a.copy()
-    oracle.reduce_local(5, 23, b, ref)
-    try:
-        for v in range(L.sosx_num_combine_variants()):
-            L.sosx_set_combine_variant(v)
-            for off in (0, 4):
-                da, pa = to_dev(torch, a, off)
-                db, pb = to_dev(torch, b, off)
-                sos.combine(5, 23, pa, pb, n)
-                torch.cuda.synchronize()
-                assert same_bits(from_dev(da, off, a), ref), (v, off)
-    finally:
-        L.sosx_set_combine_variant(0)
-
-
 def test_combine_host_pipeline_release_and_regrow(torch_cuda, sos, oracle):
     """The host pipeline's HBM slots: grown for a large chunk, reused for a smaller one,
     released (sosx_combine_host_release, as shmem_finalize does) and set up again --

@@ -98,6 +98,25 @@ def test_p2p_wait_is_bounded(signal):
     assert time.monotonic() - t0 < 55, "the job outlived the late PE's sleep"
 
 
+def test_p2p_stall_mid_call_costs_one_timeout():
+    """A peer that stops after a call's entry boundary (test hook SOSX_P2P_TEST_STALL_PE):
+    the waiting PEs' device waits time out in the call's first device step, and the
+    call's two later device steps give up at once instead of each waiting out
+    SHMEMX_P2P_TIMEOUT again (one timeout per call, not one per step)."""
+    T = 5
+    r = oshrun(4, [sys.executable, os.path.join(ROOT, "tests", "p2p_stall_pe.py")], timeout=150,
+               extra_env={"SHMEMX_P2P_TIMEOUT": str(T), "SHMEMX_P2P_SIGNAL": "stream",
+                          "SOSX_P2P_TEST_STALL_PE": "1"})
+    t_end = time.time()
+    assert r.returncode != 0, r.stdout
+    assert "timed out" in r.stderr and "device wait" in r.stderr, r.stderr[-2000:]
+    assert "reduction returned" not in r.stdout
+    starts = [float(x) for x in re.findall(r"call starts at ([\d.]+)", r.stdout)]
+    assert len(starts) == 4, r.stdout
+    # one timeout (+ launch, abort and teardown slack); three would be >= 15 s
+    assert t_end - max(starts) < 2 * T + 1, (t_end - max(starts), r.stderr[-2000:])
+
+
 @pytest.mark.parametrize("np_", [1, 2, 3, 4, 6])
 def test_team_management(np_):
     """split_strided / split_2d / team-slot pool / translate / config (tools/team_mgmt_check.py)."""

@@ -191,6 +191,17 @@ def test_error_aborts_like_sos():
              "S.shmem_int_sum_reduce(S.team_world(), a.ctypes.data + 4, a.ctypes.data, 4)\n")
     r = _run(["python", "-c", code2], env={"PYTHONPATH": ROOT})
     assert r.returncode == 1 and "overlaps" in r.stderr
+    # logPE_stride outside [0, 30]: SOS shifts 1 << logPE_stride unchecked (undefined)
+    for bad in ("4, 0, 31, 1,", "4, 0, -1, 1,"):
+        r = _run(["python", "-c", code.replace("4, 0, 0, 5,", bad)], env={"PYTHONPATH": ROOT})
+        assert r.returncode == 1 and "Invalid active set" in r.stderr and "logPE_stride" in r.stderr, \
+            r.stderr[-2000:]
+    # nreduce * sizeof(T) past SIZE_MAX: refused, not wrapped into a small size
+    code3 = ("import numpy as np\nfrom sos_amd import shmem as S\nS.shmem_init()\n"
+             "a = np.zeros(8, np.int32)\n"
+             "S.shmem_int_sum_reduce(S.team_world(), a.ctypes.data, a.ctypes.data, (1 << 63) + 1)\n")
+    r = _run(["python", "-c", code3], env={"PYTHONPATH": ROOT})
+    assert r.returncode == 1 and "overflows" in r.stderr, r.stderr[-2000:]
 
 
 def test_init_attr_one_pe():

@@ -24,10 +24,10 @@ def main():
     ap.add_argument("--op", default="sum")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--fold-ab", action="store_true",
-                    help="interleaved A/B of the fold variants (sosx_set_fold_variant) on P "
+                    help="interleaved A/B of the 8-input fold shapes (tools/variants) on P "
                          "resident chunks of n/P elements")
     ap.add_argument("--prefix-ab", action="store_true",
-                    help="interleaved A/B of the scan prefix variants (sosx_set_prefix_variant) "
+                    help="interleaved A/B of the scan prefix shapes (tools/variants) "
                          "on P resident chunks of n/P elements")
     a = ap.parse_args()
     if a.fold_ab:
@@ -89,12 +89,14 @@ def fold_ab(a, rounds=9, reps=20):
     import random
     import torch
     from sos_amd import _lib as L
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "variants"))
+    import variants as V
     torch.cuda.set_device(0)
-    dt, op = L.dtype_id(a.dtype), L.op_id(a.op)
+    a.P, a.dtype, a.op = 8, "float", "sum"      # the variant library's fold: 8 inputs, fp32 sum
+    dt = L.dtype_id(a.dtype)
     es = L.dtype_size(dt)
     chunk = a.n // a.P
-    names = ("u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd")
-    lib = L.lib()
+    names = V.names("fold")
     rng = random.Random(99)
     res = {v: [] for v in range(len(names))}
     same = True
@@ -108,13 +110,12 @@ def fold_ab(a, rounds=9, reps=20):
             L.fill(dt, 0, 0x5EED, k, x, chunk)
         ref = None
         for v in range(len(names)):
-            lib.sosx_set_fold_variant(v)
             for _ in range(3):
-                L.fold(op, dt, L.ORDER_LINEAR, out, ins, chunk)
+                V.fold(v, out, ins, chunk)
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
             for _ in range(reps):
-                L.fold(op, dt, L.ORDER_LINEAR, out, ins, chunk)
+                V.fold(v, out, ins, chunk)
             s1.record()
             torch.cuda.synchronize()
             res[v].append(s0.elapsed_time(s1) / reps)
@@ -123,7 +124,6 @@ def fold_ab(a, rounds=9, reps=20):
                 ref = last
             else:
                 same &= torch.equal(ref, last)
-        lib.sosx_set_fold_variant(0)
         del bufs, ref, last
     algo = (a.P + 1) * chunk * es
     rows = {}
@@ -145,12 +145,14 @@ def prefix_ab(a, rounds=9, reps=20):
     import random
     import torch
     from sos_amd import _lib as L
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "variants"))
+    import variants as V
     torch.cuda.set_device(0)
+    a.dtype, a.op = "float", "sum"              # the variant library's prefix: fp32 sum
     dt = L.dtype_id(a.dtype)
     es = L.dtype_size(dt)
     chunk = a.n // a.P
-    names = ("u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain", "u8_nt")
-    lib = L.lib()
+    names = V.names("prefix")
     rng = random.Random(1234)
     res = {v: [] for v in range(len(names))}
     same = True
@@ -164,13 +166,12 @@ def prefix_ab(a, rounds=9, reps=20):
             L.fill(dt, 0, 0x5EED, k, x, chunk)
         ref = None
         for v in range(len(names)):
-            lib.sosx_set_prefix_variant(v)
             for _ in range(3):
-                L.prefix(a.op, dt, op_, ip, chunk, -1)
+                V.prefix(v, op_, ip, chunk)
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
             for _ in range(reps):
-                L.prefix(a.op, dt, op_, ip, chunk, -1)
+                V.prefix(v, op_, ip, chunk)
             s1.record()
             torch.cuda.synchronize()
             res[v].append(s0.elapsed_time(s1) / reps)
@@ -179,7 +180,6 @@ def prefix_ab(a, rounds=9, reps=20):
                 ref = last
             else:
                 same &= torch.equal(ref, last)
-        lib.sosx_set_prefix_variant(0)
         del bufs, ref, last
     algo = 2 * a.P * chunk * es
     rows = {}

@@ -1,0 +1,396 @@
+// variants.hip -- BENCH-ONLY library (tools/variants/libsos_variants.so): the kernel
+// shapes the product defaults were chosen against, kept so the
+// A/Bs can be re-run and so tests can prove every shape computes the same bits.  The
+// product library (sos_amd/libsos_amd.so) contains only the defaults; nothing in it
+// calls or links this file.  fp32 sum only (the headline op):
+//   sosxv_combine : the local combine out = a + b, 20 shapes (0 = the product default)
+//   sosxv_fold    : the 8-input LINEAR fold, 8 shapes (0 = the product default)
+//   sosxv_prefix  : the 2..8-input prefix, 6 shapes (0 = the product default)
+#include "combine_kernels.h"
+#include "fold_kernels.h"
+
+namespace sos {
+
+// Buffer-descriptor variant: raw_buffer_load/store_b128 with explicit cache-policy
+// bits (gfx950 aux: sc0 = 1, nt = 2, sc1 = 16), one wave-uniform descriptor per tile.
+// Tuning variants only (tools/variants_bench.py).
+template <class T, class OP, int U, int AUXL, int AUXS>
+__global__ __launch_bounds__(kThreads) void k_combine3_buf(T *out, const T *a,
+                                                             const T *b, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    constexpr int kTileBytes = kThreads * U * 16;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t tb = t * (size_t)kTileBytes;
+        auto rA = __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)(a + g.head) + tb), 0,
+                                                    kTileBytes, 0x00020000);
+        auto rB = __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)(b + g.head) + tb), 0,
+                                                    kTileBytes, 0x00020000);
+        auto rO = __builtin_amdgcn_make_buffer_rsrc((void *)((char *)(out + g.head) + tb), 0,
+                                                    kTileBytes, 0x00020000);
+        u32x4 ra[U], rb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int off = (int)(threadIdx.x + u * kThreads) * 16;
+            ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rA, off, 0, AUXL);
+            rb[u] = __builtin_amdgcn_raw_buffer_load_b128(rB, off, 0, AUXL);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(apply<T, OP>(ra[u], rb[u]), rO,
+                                                   (int)(threadIdx.x + u * kThreads) * 16, 0, AUXS);
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n;
+             i += kThreads)
+            out[i] = OP::f(a[i], b[i]);
+    }
+}
+
+// LDS-staged partner tile: the partner vector `b` is brought into LDS by LDS-DMA
+// (global_load_lds_dwordx4) while `a` streams into registers.  Kept as a measured
+// alternative (tools/variants_bench.py); for a pure 3-stream combine the LDS round trip
+// buys nothing over register staging (MI355X guide, "glds vs register staging").
+template <class T, class OP, int U>
+__global__ __launch_bounds__(kThreads) void k_combine3_lds(T *out, const T *a,
+                                                             const T *b, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    __shared__ __attribute__((aligned(16))) u32x4 tile[kThreads * U];
+    const u32x4 *A = reinterpret_cast<const u32x4 *>(a + g.head);
+    const u32x4 *B = reinterpret_cast<const u32x4 *>(b + g.head);
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t base = t * (size_t)(kThreads * U) + threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            // LDS destination = wave-uniform base + lane*16 (lane-linear image).
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(B + base + u * kThreads),
+                (__attribute__((address_space(3))) void *)(&tile[u * kThreads + wave * 64]), 16,
+                0, 0);
+        }
+        u32x4 ra[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) ra[u] = A[base + u * kThreads];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            O[base + u * kThreads] = apply<T, OP>(ra[u], tile[u * kThreads + wave * 64 + lane]);
+        __builtin_amdgcn_s_barrier();
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n;
+             i += kThreads)
+            out[i] = OP::f(a[i], b[i]);
+    }
+}
+
+// Shape experiments (tools/variants_bench.py): TPB threads per workgroup (tile = TPB 16-B
+// vectors per operand) and, with XCD = 1, an XCD-contiguous tile order: the dispatcher
+// deals consecutive workgroups round-robin to the 8 XCDs, so workgroup w runs on XCD
+// w % 8; tile = (w % 8) * per_xcd + w / 8 gives each XCD one contiguous stretch of the
+// vectors instead of every 8th tile.
+template <class T, class OP, int TPB, int XCD>
+__global__ __launch_bounds__(TPB) void k_combine3_x(T *out, const T *a, const T *b, Geom g,
+                                                   unsigned nvec_tiles)
+{
+    constexpr int V = Pack<T>::N;
+    const u32x4 *A = reinterpret_cast<const u32x4 *>(a + g.head);
+    const u32x4 *B = reinterpret_cast<const u32x4 *>(b + g.head);
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    const unsigned w = blockIdx.x;
+    if (w < nvec_tiles) {
+        size_t t = w;
+        if constexpr (XCD) {
+            const unsigned per = nvec_tiles / 8;   // host guarantees nvec_tiles % 8 == 0
+            t = (size_t)(w % 8) * per + w / 8;
+        }
+        const size_t i = t * TPB + threadIdx.x;
+        u32x4 ra = ldv<true>(A + i), rb = ldv<true>(B + i);
+        stv<true>(O + i, apply<T, OP>(ra, rb));
+    } else if (g.has_rem && threadIdx.x < kThreads) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
+        for (size_t i = g.head + (size_t)nvec_tiles * TPB * V + threadIdx.x; i < g.n; i += kThreads)
+            out[i] = OP::f(a[i], b[i]);
+    }
+}
+
+// Tuning variants of k_fold (bench A/B, sosxv_fold): each workgroup takes S
+// consecutive tiles (longer contiguous runs per input stream), optionally loading tile
+// j+1 before storing tile j (PF), optionally with an XCD-contiguous tile order
+// (workgroup w runs on XCD w % 8).  Same element order as k_fold.
+template <class T, class OP, int NP, int ORDER, int S, bool PF, bool XCD>
+__global__ __launch_bounds__(kThreads) void k_fold_st(T *out, FoldPtrs ins, Geom g, size_t groups)
+{
+    constexpr int V = Pack<T>::N;
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    size_t grp = blockIdx.x;
+    if (XCD && groups % 8 == 0 && grp < groups) grp = (grp % 8) * (groups / 8) + grp / 8;
+    if (grp < groups) {
+        const size_t t0 = grp * S;
+        const size_t t1 = t0 + S < g.tiles ? t0 + S : g.tiles;
+        u32x4 x[NP];
+        auto load = [&](size_t t, u32x4 (&d)[NP]) {
+            const size_t i = t * (size_t)kThreads + threadIdx.x;
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                d[k] = ldv<true>(reinterpret_cast<const u32x4 *>((const T *)ins.p[k] + g.head) + i);
+        };
+        if (PF) {
+            load(t0, x);
+            for (size_t t = t0; t < t1; ++t) {
+                u32x4 y[NP];
+                if (t + 1 < t1) load(t + 1, y);
+                stv<true>(O + t * (size_t)kThreads + threadIdx.x, fold_pack<T, OP, NP, ORDER>(x));
+#pragma unroll
+                for (int k = 0; k < NP; ++k) x[k] = y[k];
+            }
+        } else {
+            for (size_t t = t0; t < t1; ++t) {
+                load(t, x);
+                stv<true>(O + t * (size_t)kThreads + threadIdx.x, fold_pack<T, OP, NP, ORDER>(x));
+            }
+        }
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)ins.p[k])[i];
+            out[i] = fold_elem<T, OP, NP, ORDER>(v);
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
+}  // namespace sos
+
+using namespace sos;
+
+namespace {
+
+using T = float;
+using OP = OpSum;
+
+const char *const kCombineNames[] = {
+    "u1_nt",             // 0: the product default: U=1, nontemporal loads+stores, one tile/workgroup
+    "u4_nt",             // 1: U=4 (round-1 default until the A/B in profiles/r1_combine_variants*)
+    "u2_nt",             // 2
+    "u8_nt",             // 3
+    "u4_ntload",         // 4: nontemporal loads, plain stores
+    "u4_plain",          // 5: plain loads/stores
+    "u1_plain",          // 6
+    "u4_nt_persist4096", // 7: grid-stride over 4096 workgroups
+    "u2_nt_persist2048", // 8
+    "u4_lds_dma",        // 9: partner tile via global_load_lds (LDS-DMA)
+    "buf_u4_nt",         // 10: buffer loads/stores, aux nt
+    "buf_u4_plainld_ntst",  // 11
+    "buf_u4_sc1nt",      // 12: aux sc1|nt both ways
+    "buf_u2_nt",         // 13
+    "buf_u1_nt",         // 14
+    "x256_xcd",          // 15: 256 threads, XCD-contiguous tiles
+    "x512",              // 16: 512 threads per workgroup (8 KiB tiles)
+    "x1024",             // 17: 1024 threads per workgroup
+    "x512_xcd",          // 18
+    "x256",              // 19: the k_combine3_x control (same shape as u1_nt)
+};
+constexpr int kNumCombine = (int)(sizeof(kCombineNames) / sizeof(kCombineNames[0]));
+
+template <int U, bool NTL, bool NTS>
+int combine_vec(T *out, const T *a, const T *b, size_t n, hipStream_t st, size_t cap)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), U);
+    hipLaunchKernelGGL((k_combine3<T, OP, U, NTL, NTS>), dim3(grid_for(g, cap)), dim3(kThreads), 0,
+                       st, out, a, b, g);
+    return hip_ok(hipGetLastError());
+}
+
+template <int TPB, int XCD>
+int combine_x(T *out, const T *a, const T *b, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), 1);
+    const size_t V = 16 / sizeof(T);
+    size_t tiles = (n - g.head) / V / TPB;
+    if (XCD) tiles -= tiles % 8;
+    g.tiles = tiles;
+    g.has_rem = (g.head > 0) || (tiles * TPB * V != n - g.head);
+    const unsigned grid = (unsigned)(tiles + (g.has_rem ? 1 : 0));
+    if (grid == 0) return SOSX_OK;
+    hipLaunchKernelGGL((k_combine3_x<T, OP, TPB, XCD>), dim3(grid), dim3(TPB), 0, st, out, a, b, g,
+                       (unsigned)tiles);
+    return hip_ok(hipGetLastError());
+}
+
+template <int U, int AUXL, int AUXS>
+int combine_buf(T *out, const T *a, const T *b, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), U);
+    hipLaunchKernelGGL((k_combine3_buf<T, OP, U, AUXL, AUXS>), dim3(grid_for(g, kNoCap)),
+                       dim3(kThreads), 0, st, out, a, b, g);
+    return hip_ok(hipGetLastError());
+}
+
+template <int NP, int U>
+int fold_u(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), U);
+    hipLaunchKernelGGL((k_fold<T, OP, NP, SOSX_ORDER_LINEAR, U>), dim3(grid_for(g, kNoCap)),
+                       dim3(kThreads), 0, st, out, ins, g);
+    return hip_ok(hipGetLastError());
+}
+
+template <int S, bool PF, bool XCD>
+int fold_st(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), 1);
+    const size_t groups = (g.tiles + S - 1) / S;
+    unsigned blocks = (unsigned)(groups + (g.has_rem ? 1 : 0));
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL((k_fold_st<T, OP, 8, SOSX_ORDER_LINEAR, S, PF, XCD>), dim3(blocks),
+                       dim3(kThreads), 0, st, out, ins, g, groups);
+    return hip_ok(hipGetLastError());
+}
+
+const char *const kFoldNames[] = {"u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd"};
+constexpr int kNumFold = 8;
+
+const char *const kPrefixNames[] = {"u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain", "u8_nt"};
+constexpr int kNumPrefix = 6;
+
+template <int NP, int U, bool NT>
+int prefix_u(const PrefixPtrs &p, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), U);
+    hipLaunchKernelGGL((k_prefix<T, OP, NP, U, NT>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0,
+                       st, p, g);
+    return hip_ok(hipGetLastError());
+}
+
+template <int NP>
+int prefix_np(int v, const PrefixPtrs &p, size_t n, hipStream_t st)
+{
+    switch (v) {
+        case 0: return prefix_u<NP, 1, true>(p, n, st);
+        case 1: return prefix_u<NP, 2, true>(p, n, st);
+        case 2: return prefix_u<NP, 4, true>(p, n, st);
+        case 3: return prefix_u<NP, 1, false>(p, n, st);
+        case 4: return prefix_u<NP, 2, false>(p, n, st);
+        case 5: return prefix_u<NP, 8, true>(p, n, st);
+    }
+    return SOSX_ERR_ARG;
+}
+
+bool congruent16(const void *const *ps, int k, uintptr_t o)
+{
+    for (int i = 0; i < k; ++i)
+        if ((((uintptr_t)ps[i]) ^ o) & 15) return false;
+    return (o % sizeof(T)) == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sosxv_num_combine(void) { return kNumCombine; }
+const char *sosxv_combine_name(int v) { return v >= 0 && v < kNumCombine ? kCombineNames[v] : ""; }
+
+// out = a + b over n fp32 elements (out may alias a); operands 16-B congruent.
+int sosxv_combine(int v, float *out, const float *a, const float *b, size_t n, void *stream)
+{
+    hipStream_t st = as_stream(stream);
+    const void *ps[2] = {a, b};
+    if (v < 0 || v >= kNumCombine || !out || !a || !b || !congruent16(ps, 2, (uintptr_t)out))
+        return SOSX_ERR_ARG;
+    if (n == 0) return SOSX_OK;
+    switch (v) {
+        case 0: return combine_vec<1, true, true>(out, a, b, n, st, kNoCap);
+        case 1: return combine_vec<4, true, true>(out, a, b, n, st, kNoCap);
+        case 2: return combine_vec<2, true, true>(out, a, b, n, st, kNoCap);
+        case 3: return combine_vec<8, true, true>(out, a, b, n, st, kNoCap);
+        case 4: return combine_vec<4, true, false>(out, a, b, n, st, kNoCap);
+        case 5: return combine_vec<4, false, false>(out, a, b, n, st, kNoCap);
+        case 6: return combine_vec<1, false, false>(out, a, b, n, st, kNoCap);
+        case 7: return combine_vec<4, true, true>(out, a, b, n, st, 4096);
+        case 8: return combine_vec<2, true, true>(out, a, b, n, st, 2048);
+        case 9: {
+            Geom g = make_geom((uintptr_t)out, n, sizeof(T), 4);
+            hipLaunchKernelGGL((k_combine3_lds<T, OP, 4>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
+                               0, st, out, a, b, g);
+            return hip_ok(hipGetLastError());
+        }
+        case 10: return combine_buf<4, 2, 2>(out, a, b, n, st);
+        case 11: return combine_buf<4, 0, 2>(out, a, b, n, st);
+        case 12: return combine_buf<4, 18, 18>(out, a, b, n, st);
+        case 13: return combine_buf<2, 2, 2>(out, a, b, n, st);
+        case 14: return combine_buf<1, 2, 2>(out, a, b, n, st);
+        case 15: return combine_x<256, 1>(out, a, b, n, st);
+        case 16: return combine_x<512, 0>(out, a, b, n, st);
+        case 17: return combine_x<1024, 0>(out, a, b, n, st);
+        case 18: return combine_x<512, 1>(out, a, b, n, st);
+        case 19: return combine_x<256, 0>(out, a, b, n, st);
+    }
+    return SOSX_ERR_ARG;
+}
+
+int sosxv_num_fold(void) { return kNumFold; }
+const char *sosxv_fold_name(int v) { return v >= 0 && v < kNumFold ? kFoldNames[v] : ""; }
+
+// out = ((ins[0] + ins[1]) + ...) + ins[7] over n fp32 elements (the ring's LINEAR fold).
+int sosxv_fold(int v, float *out, const void *const *ins, size_t n, void *stream)
+{
+    hipStream_t st = as_stream(stream);
+    if (v < 0 || v >= kNumFold || !out || !ins || !congruent16(ins, 8, (uintptr_t)out))
+        return SOSX_ERR_ARG;
+    if (n == 0) return SOSX_OK;
+    FoldPtrs fp;
+    memset(&fp, 0, sizeof(fp));
+    for (int k = 0; k < 8; ++k) fp.p[k] = ins[k];
+    switch (v) {
+        case 0: return fold_u<8, 1>(out, fp, n, st);
+        case 1: return fold_u<8, 2>(out, fp, n, st);
+        case 2: return fold_u<8, 4>(out, fp, n, st);
+        case 3: return fold_st<4, false, false>(out, fp, n, st);
+        case 4: return fold_st<16, false, false>(out, fp, n, st);
+        case 5: return fold_st<1, false, true>(out, fp, n, st);
+        case 6: return fold_st<4, true, false>(out, fp, n, st);
+        case 7: return fold_st<16, true, true>(out, fp, n, st);
+    }
+    return SOSX_ERR_ARG;
+}
+
+int sosxv_num_prefix(void) { return kNumPrefix; }
+const char *sosxv_prefix_name(int v) { return v >= 0 && v < kNumPrefix ? kPrefixNames[v] : ""; }
+
+// outs[k] = ins[0] + ... + ins[k], k < np (2..8), over n fp32 elements.
+int sosxv_prefix(int v, void *const *outs, const void *const *ins, int np, size_t n, void *stream)
+{
+    hipStream_t st = as_stream(stream);
+    if (v < 0 || v >= kNumPrefix || np < 2 || np > 8 || !outs || !ins) return SOSX_ERR_ARG;
+    const uintptr_t o = (uintptr_t)outs[0];
+    if (!congruent16(ins, np, o) || !congruent16((const void *const *)outs, np, o)) return SOSX_ERR_ARG;
+    if (n == 0) return SOSX_OK;
+    PrefixPtrs pp;
+    memset(&pp, 0, sizeof(pp));
+    for (int k = 0; k < np; ++k) {
+        pp.in[k] = ins[k];
+        pp.out[k] = outs[k];
+    }
+    switch (np) {
+        case 2: return prefix_np<2>(v, pp, n, st);
+        case 3: return prefix_np<3>(v, pp, n, st);
+        case 4: return prefix_np<4>(v, pp, n, st);
+        case 5: return prefix_np<5>(v, pp, n, st);
+        case 6: return prefix_np<6>(v, pp, n, st);
+        case 7: return prefix_np<7>(v, pp, n, st);
+        case 8: return prefix_np<8>(v, pp, n, st);
+    }
+    return SOSX_ERR_ARG;
+}
+
+}  // extern "C"
