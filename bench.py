@@ -35,10 +35,6 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-if os.environ.get("SOSX_CRASHTRACE") == "1":  # diagnostics only: native crash dump
-    import ctypes
-    ctypes.CDLL(os.path.join(HERE, "tools", "diag", "libcrashtrace.so"))
-
 GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 SEED = 0x5EED

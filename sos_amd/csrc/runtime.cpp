@@ -2,6 +2,7 @@
 // the MI355X SOS reduction runtime.  See runtime.h for the design.
 #include "runtime.h"
 
+#include <execinfo.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -40,6 +41,28 @@ State &st()
 // ---------------------------------------------------------------------------------
 // diagnostics (src/shmem_internal.h:60-180)
 // ---------------------------------------------------------------------------------
+// SHMEM_BACKTRACE (src/backtrace.c:181-206): "" (default) off, "execinfo" or "auto" the
+// glibc backtrace of the failing PE on stderr; "gdb" is not offered by this build (a
+// debugger attached to a process holding a GPU context is not something to start from
+// an abort path), and any other value is ignored with SOS's warning.
+static void print_backtrace()
+{
+    const char *m = getenv("SHMEM_BACKTRACE");
+    if (!m) m = getenv("SMA_BACKTRACE");
+    if (!m || !*m) return;
+    if (strcmp(m, "execinfo") && strcmp(m, "auto")) {
+        if (!strcmp(m, "gdb"))
+            fprintf(stderr, "[%04d] WARN:  Backtrace support through gdb is not available.\n", st().my_pe);
+        else
+            fprintf(stderr, "[%04d] WARN:  Ignoring invalid backtrace method '%s'.\n", st().my_pe, m);
+        return;
+    }
+    void *frames[64];
+    const int n = backtrace(frames, 64);
+    fprintf(stderr, "[%04d] backtrace (%d frames):\n", st().my_pe, n);
+    backtrace_symbols_fd(frames, n, 2);
+}
+
 void raise_error(const char *fmt, ...)
 {
     char buf[1024];
@@ -48,6 +71,7 @@ void raise_error(const char *fmt, ...)
     vsnprintf(buf, sizeof(buf), fmt, ap);
     va_end(ap);
     fprintf(stderr, "[%04d] ERROR: %s\n", st().my_pe, buf);
+    print_backtrace();
     fprintf(stderr, "[%04d] ERROR: Sandia OpenSHMEM (MI355X reduction path) exited in error\n",
             st().my_pe);
     fflush(stderr);
@@ -131,6 +155,66 @@ int parse_reduce_alg(const char *type, int dflt)
     if (!strcmp(type, "recdbl_gather")) return SOSX_ALG_RECDBL_GATHER;
     warn("Ignoring bad reduction algorithm '%s'", type);
     return dflt;
+}
+
+// SHMEM_INFO / SHMEM_VERSION (src/init.c:240-255, src/shmem_env.c:177-220): PE 0 prints
+// the package string, and with SHMEM_INFO the parameters this build reads, in SOS's
+// format: name, current value, kind, default, description.
+struct EnvDef {
+    const char *name, *kind, *dflt, *cat, *desc;
+};
+static const EnvDef kEnv[] = {
+    {"SHMEM_INFO", "bool", "false", "openshmem", "Print library information message at startup"},
+    {"SHMEM_VERSION", "bool", "false", "openshmem", "Print library version at startup"},
+    {"SHMEM_DEBUG", "bool", "false", "openshmem", "Enable debugging messages"},
+    {"SHMEM_SYMMETRIC_SIZE", "size", "536870912", "openshmem", "Symmetric heap size (pinned host memory)"},
+    {"SHMEM_TEAMS_MAX", "long", "10", "other", "Maximum number of teams per PE"},
+    {"SHMEM_BACKTRACE", "string", "", "other", "Method for backtraces on error (execinfo, auto)"},
+    {"SHMEM_COLL_SIZE_CROSSOVER", "size", "16384", "collectives",
+     "Crossover between latency and bandwidth optimized collectives (msg. size)"},
+    {"SHMEM_REDUCE_ALGORITHM", "string", "auto", "collectives",
+     "Algorithm for reductions.  Options are auto, linear, tree, recdbl, ring, rechalving, "
+     "recdbl_direct, recdbl_gather"},
+    {"SHMEMX_TRANSPORT", "string", "rccl", "device", "Inter-PE transport: rccl, p2p or both"},
+    {"SHMEMX_DEVICE", "long", "local rank % GPUs", "device", "GPU of this PE"},
+    {"SHMEMX_DEVICE_HEAP_SIZE", "size", "2147483648", "device", "Device symmetric heap size (HBM)"},
+    {"SHMEMX_STAGE_BYTES", "size", "536870912", "device",
+     "Stage region of the device heap (host operands, p2p exchange scratch)"},
+    {"SHMEMX_HEAP_ON_DEVICE", "bool", "false", "device", "shmem_malloc returns device memory"},
+    {"SHMEMX_CHECK_SYMMETRIC", "bool", "false", "device", "Check that collective buffers are symmetric"},
+    {"SHMEMX_HOST_STRIPE_BYTES", "size", "262144", "device",
+     "Slice size of the striped host-resident ring (H2D || exchange || D2H)"},
+    {"SHMEMX_RCCL_ALLGATHER", "long", "0", "device", "1: equal-chunk allgather rounds as ncclAllGather"},
+    {"SHMEMX_RCCL_ALLREDUCE", "long", "0", "device",
+     "1: integer world reductions as ncclAllReduce; 2: also fp sum/prod (RCCL's order)"},
+    {"SHMEMX_P2P_SIGNAL", "string", "stream on one GPU, host across GPUs", "device",
+     "p2p round signalling: stream (device) or host"},
+    {"SHMEMX_P2P_TIMEOUT", "long", "300", "device", "Seconds before a p2p wait ends the job"},
+};
+
+static void print_env()
+{
+    static const struct { const char *cat, *title; } sections[] = {
+        {"openshmem", nullptr}, {"other", "Additional options"},
+        {"collectives", "Collectives options"}, {"device", "MI355X (HIP / RCCL) options"}};
+    for (const auto &sec : sections) {
+        if (sec.title) printf("\n%s:\n", sec.title);
+        for (const EnvDef &e : kEnv) {
+            if (strcmp(e.cat, sec.cat)) continue;
+            const char *v = getenv(e.name);
+            if (!v && !strncmp(e.name, "SHMEM_", 6)) v = getenv((std::string("SMA_") + (e.name + 6)).c_str());
+            printf("  %-27s %s (type: %s, default: %s)\n\t%s\n", e.name, v ? v : e.dflt, e.kind,
+                   e.dflt, e.desc);
+        }
+    }
+    printf("\nNetwork transport: none (intra-node: RCCL over xGMI / IPC-mapped HBM)\n\n");
+    fflush(stdout);
+}
+
+static bool env_flag(const char *name)
+{
+    const char *v = getenv2(name);
+    return v && *v && strcmp(v, "0") && strcasecmp(v, "false") && strcasecmp(v, "no");
 }
 
 static void read_env(State &s)
@@ -366,6 +450,15 @@ void *stage(size_t bytes) { return grow(&st().stage, &st().stage_bytes, bytes, "
 bool is_device_ptr(const void *p)
 {
     if (!p) return false;
+    // the symmetric regions this library created answer without a runtime query (a
+    // hipPointerGetAttributes costs about a microsecond; every call asks for two)
+    State &s = st();
+    const char *c = (const char *)p;
+    if (s.dev_heap.contains(p, 1) || (s.sym_stage && c >= s.sym_stage && c < s.sym_stage + s.sym_stage_bytes))
+        return true;
+    if (s.ext_base && c >= (char *)s.ext_base && c < (char *)s.ext_base + s.ext_size) return true;
+    if (s.host_heap.contains(p, 1)) return false;
+    if (__data_start && _end && c >= __data_start && c < _end) return false;
     hipPointerAttribute_t a;
     hipError_t e = hipPointerGetAttributes(&a, p);
     if (e != hipSuccess) {
@@ -488,6 +581,11 @@ static void init_common(int pe, int npes, const ncclUniqueId *uid)
     s.initialized = true;
     s.finalized = false;
     if (s.want_p2p || s.ext_base) ensure_device_heap();
+    if (pe == 0 && (env_flag("VERSION") || env_flag("INFO") || s.debug)) {
+        printf("Sandia OpenSHMEM 1.5.3 (MI355X reduction path, libsos_amd)\n");
+        if (env_flag("INFO")) print_env();
+        fflush(stdout);
+    }
     debug_msg("PE %d of %d on device %d, transport %s, reduce algorithm %d, crossover %zu", pe,
               npes, s.device, s.transport == TRANSPORT_P2P ? "p2p" : "rccl", s.reduce_alg,
               s.coll_size_crossover);

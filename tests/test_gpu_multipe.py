@@ -206,7 +206,7 @@ def test_p2p_stage_overflow_is_an_error(tmp_path):
 @pytest.mark.parametrize("heap", ["2G", "3400M"])
 def test_ipc_heap_sizes_with_bit31(heap):
     """torch's HIP 7.0.2 hangs in hipIpcOpenMemHandle for exported sizes with bit 31 set;
-    the library rounds such heaps up (tests/heap_init_pe.py, tools/diag/heap_probe.c on /opt/rocm 7.2 maps them all)."""
+    the library rounds such heaps up (tests/heap_init_pe.py; /opt/rocm 7.2 maps them all)."""
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)

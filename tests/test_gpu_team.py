@@ -204,6 +204,26 @@ def test_error_aborts_like_sos():
     assert r.returncode == 1 and "overflows" in r.stderr, r.stderr[-2000:]
 
 
+def test_info_and_backtrace_env():
+    """SHMEM_INFO prints the package string and the parameter table on PE 0 at init
+    (src/init.c:240-255, src/shmem_env.c:177-220); SHMEM_BACKTRACE=execinfo adds the
+    failing PE's backtrace to an abort (src/backtrace.c:181-206)."""
+    code = ("from sos_amd import shmem as S\nS.shmem_init()\nS.shmem_finalize()\n")
+    r = _run(["python", "-c", code], env={"PYTHONPATH": ROOT, "SHMEM_INFO": "1",
+                                          "SHMEM_REDUCE_ALGORITHM": "ring"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Sandia OpenSHMEM" in r.stdout
+    line = next(ln for ln in r.stdout.splitlines() if "SHMEM_REDUCE_ALGORITHM" in ln)
+    assert " ring (type: string, default: auto)" in line, line
+    assert "Collectives options:" in r.stdout and "SHMEMX_TRANSPORT" in r.stdout
+    bad = ("import numpy as np\nfrom sos_amd import shmem as S\nS.shmem_init()\n"
+           "a = np.zeros(4, np.int32)\n"
+           "S.shmem_int_sum_to_all(a.ctypes.data, a.ctypes.data, 4, 0, 0, 5, None, None)\n")
+    r = _run(["python", "-c", bad], env={"PYTHONPATH": ROOT, "SHMEM_BACKTRACE": "execinfo"})
+    assert r.returncode == 1 and "Invalid active set" in r.stderr
+    assert "backtrace (" in r.stderr and "libsos_amd.so" in r.stderr, r.stderr[-2000:]
+
+
 def test_init_attr_one_pe():
     """shmemx_get_unique_id + shmemx_init_attr (no TCP bootstrap, no node shared memory):
     a reduction, a team split (agreement path without shm) and finalize."""

@@ -1,49 +1,145 @@
-"""Small-message team-reduction latency per schedule (run under tools/oshrun).
+"""Small-message team-reduction latency (run under tools/oshrun -np P).
 
-Every PE times `reps` back-to-back shmem_float_sum_reduce(SHMEM_TEAM_WORLD) calls on
-device-heap buffers for each schedule and size; PE 0 prints microseconds per call
-(the calls are collective, so PE 0's time is the team's).  Used to compare recdbl_sw's
-log2(P)-round butterfly with its one-round gather form (SOSX_ALG_RECDBL_GATHER), and the
-p2p transport's signalling modes (SHMEMX_P2P_SIGNAL=stream|host) from 4 B to 4 MiB.
+Every PE times `reps` back-to-back shmem_float_sum_reduce(SHMEM_TEAM_WORLD) calls per
+schedule and size; PE 0 prints microseconds per call, the max over PEs (the calls are
+collective).  Legs:
+  dev   : operands in the device symmetric heap (shmemx_malloc_device)
+  host  : operands in the host symmetric heap (shmem_malloc: pinned host memory, SOS's
+          own case -- the reductions below COLL_SIZE_CROSSOVER that SOS runs on the CPU)
+  cpu   : SOS's own CPU recdbl_sw (oracle/sos_oracle.c oracle_pe_recdbl,
+          src/collectives.c:850-984), one pinned core per PE, memcpy puts and flag stores
+          over a /dev/shm segment (the XPMEM model), on the same P processes, one
+          barrier per call (the team API's pSync reuse rule) -- the reference baseline
+Schedules: recdbl (recdbl_sw butterfly), recdbl_gather (one all-gather round + every
+PE's own tree: AUTO below the crossover), ring (AUTO above it).
 """
+import argparse
+import ctypes
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
 
 from sos_amd import _lib as L  # noqa: E402
 from sos_amd import shmem as S  # noqa: E402
 
+SMALL = [1, 64, 1024, 4095]      # fp32: up to 16380 B, below the 16 KiB crossover
+
+
+def max_over_pes(v, scratch):
+    """Max of a float over all PEs, through the library's own double max reduce."""
+    a = np.ctypeslib.as_array((ctypes.c_double * 2).from_address(scratch))
+    a[0] = v
+    S.shmem_double_max_reduce(S.team_world(), scratch + 8, scratch, 1)
+    return float(a[1])
+
+
+def time_calls(fn, reps):
+    for _ in range(10):
+        fn()
+    S.shmem_barrier_all()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return (time.perf_counter() - t0) / reps
+
+
+def cpu_leg(me, P, reps, scratch):
+    """SOS's recdbl_sw on the CPU, one pinned physical core per PE."""
+    from oracle import oracle as O
+    allowed = sorted(os.sched_getaffinity(0))
+    prim = []
+    for c in allowed:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                first = int(f.read().replace("-", ",").split(",")[0])
+        except (OSError, ValueError):
+            first = c
+        if first == c or first not in allowed:
+            prim.append(c)
+    path = f"/dev/shm/sosx_lat_{os.getppid()}_{P}"
+    nmax = max(SMALL)
+    if me == 0:
+        if os.path.exists(path):
+            os.unlink(path)
+        ring = O.PeRing(path, P, 0, nmax, 23, create=True, alg="recdbl")
+    S.shmem_barrier_all()
+    if me != 0:
+        ring = O.PeRing(path, P, me, nmax, 23, create=False, alg="recdbl")
+    S.shmem_barrier_all()
+    if me == 0:
+        os.unlink(path)
+    src = O.fill(23, 0, 7, me, nmax)
+    out = {}
+    os.sched_setaffinity(0, {prim[me % len(prim)]})
+    try:
+        for n in SMALL:
+            ring.count = n
+            ring.time(5, src, 100)                 # warm-up
+            t = ring.time(5, src, reps) / reps
+            out[n] = t
+    finally:
+        os.sched_setaffinity(0, set(allowed))
+    S.shmem_barrier_all()
+    ring.close()
+    return {n: max_over_pes(t, scratch) for n, t in out.items()}, prim[0]
+
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--legs", default="dev,host,cpu")
+    ap.add_argument("--reps", type=int, default=int(os.environ.get("LAT_REPS", "200")))
+    ap.add_argument("--ring", action="store_true", help="also the ring above the crossover (dev)")
+    a = ap.parse_args()
     S.shmem_init()
     me, P = S.shmem_my_pe(), S.shmem_n_pes()
-    sizes = [1, 64, 1024, 4095]
+    legs = a.legs.split(",")
+    team = S.team_world()
     ring_sizes = [16384, 262144, 1 << 20]
     nmax = max(ring_sizes)
-    src = S.shmemx_malloc_device(nmax * 4)
-    dst = S.shmemx_malloc_device(nmax * 4)
-    L.fill(23, 0, 7, me, src, nmax)
-    team = S.team_world()
-    reps = int(os.environ.get("LAT_REPS", "200"))
-    for alg, ns in (("recdbl", sizes), ("recdbl_gather", sizes), ("ring", ring_sizes)):
-        S.shmemx_set_reduce_algorithm(L.ALGS[alg])
-        for n in ns:
-            for _ in range(10):
-                S.shmem_float_sum_reduce(team, dst, src, n)
-            S.shmem_barrier_all()
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                S.shmem_float_sum_reduce(team, dst, src, n)
-            t = (time.perf_counter() - t0) / reps
-            if me == 0:
-                print(f"P={P} {alg:14s} n={n:7d}: {t * 1e6:8.1f} us/call", flush=True)
+    scratch = S.lib().shmem_malloc(64)
+    rows = []
+    if "dev" in legs:
+        src = S.shmemx_malloc_device(nmax * 4)
+        dst = S.shmemx_malloc_device(nmax * 4)
+        L.fill(23, 0, 7, me, src, nmax)
+        plan = [("recdbl", SMALL), ("recdbl_gather", SMALL)] + ([("ring", ring_sizes)] if a.ring else [])
+        for alg, ns in plan:
+            S.shmemx_set_reduce_algorithm(L.ALGS[alg])
+            for n in ns:
+                t = time_calls(lambda: S.shmem_float_sum_reduce(team, dst, src, n), a.reps)
+                rows.append(("dev", alg, n, max_over_pes(t, scratch)))
+        S.shmemx_free_device(dst)
+        S.shmemx_free_device(src)
+    if "host" in legs:
+        hs = S.lib().shmem_malloc(max(SMALL) * 4)
+        hd = S.lib().shmem_malloc(max(SMALL) * 4)
+        np.ctypeslib.as_array((ctypes.c_float * max(SMALL)).from_address(hs))[:] = 0.5 + me
+        for alg in ("recdbl", "recdbl_gather"):
+            S.shmemx_set_reduce_algorithm(L.ALGS[alg])
+            for n in SMALL:
+                t = time_calls(lambda: S.shmem_float_sum_reduce(team, hd, hs, n), a.reps)
+                rows.append(("host", alg, n, max_over_pes(t, scratch)))
+        S.lib().shmem_free(hd)
+        S.lib().shmem_free(hs)
+    S.shmemx_set_reduce_algorithm(L.ALGS["auto"])
+    if "cpu" in legs:
+        cpu, core0 = cpu_leg(me, P, max(a.reps * 10, 2000), scratch)
+        for n, t in cpu.items():
+            rows.append(("cpu", "recdbl_sw", n, t))
+    if me == 0:
+        for leg, alg, n, t in rows:
+            print(f"P={P} {leg:4s} {alg:14s} n={n:7d}: {t * 1e6:8.2f} us/call", flush=True)
+        if "cpu" in legs:
+            print(f"# cpu: oracle_pe_recdbl, {P} processes pinned to consecutive physical cores "
+                  f"from {core0}, barrier per call included", flush=True)
     S.shmem_barrier_all()
-    S.shmemx_free_device(dst)
-    S.shmemx_free_device(src)
+    S.lib().shmem_free(scratch)
     S.shmem_finalize()
     return 0
 
