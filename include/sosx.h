@@ -196,6 +196,11 @@ int sosx_set_rccl_allreduce(int mode);
  * device heap. */
 void sosx_p2p_flags(unsigned *host_register, unsigned *ipc_open);
 
+/* Team reductions that took the small host-resident path (operands in host memory,
+ * recdbl_sw semantics, at most 64 KiB: node shared memory + one fold kernel reading
+ * every PE's operand in place).  Introspection for tests and benchmarks. */
+long sosx_small_path_calls(void);
+
 /* Library / build identification. */
 const char *sosx_build_info(void);
 

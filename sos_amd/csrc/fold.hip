@@ -96,13 +96,20 @@ using namespace sos;
 
 namespace {
 
+// Inputs of at most this many bytes each are folded one element per lane: the grid then
+// has n/256 workgroups instead of n/(256*U*V), so a small fold whose inputs sit in host
+// memory (the small host-resident path, smallpath.cpp) or behind xGMI has many
+// workgroups' loads in flight at once instead of one workgroup's; latency, not
+// bandwidth, bounds these calls.
+constexpr size_t kSpreadBytes = 64 * 1024;
+
 template <class T, class OP, int NP, int ORDER>
 int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 {
     uintptr_t o = (uintptr_t)out;
     bool congruent = (o % sizeof(T)) == 0 && sizeof(T) <= 16;
     for (int k = 0; k < NP; ++k) congruent &= (((uintptr_t)ins.p[k] ^ o) & 15) == 0;
-    if (!congruent) {
+    if (!congruent || n * sizeof(T) <= kSpreadBytes) {
         size_t blocks = (n + kThreads - 1) / kThreads;
         if (blocks > 8192) blocks = 8192;
         hipLaunchKernelGGL((k_fold_scalar<T, OP, NP, ORDER>), dim3((unsigned)blocks),

@@ -517,6 +517,10 @@ Team *team_from_handle(shmem_team_t handle) { return reinterpret_cast<Team *>(ha
 // ---------------------------------------------------------------------------------
 // init (src/init.c:221-567, condensed to what the reduction path needs)
 // ---------------------------------------------------------------------------------
+// The shared segment's p2p region, rounded to whole pages (the small-path region
+// follows it, so the two HIP registrations never share a page).
+static size_t shm_p2p_region_bytes() { return (p2p_shared_bytes() + 4095) & ~(size_t)4095; }
+
 static void init_common(int pe, int npes, const ncclUniqueId *uid)
 {
     State &s = st();
@@ -581,6 +585,8 @@ static void init_common(int pe, int npes, const ncclUniqueId *uid)
     s.initialized = true;
     s.finalized = false;
     if (s.want_p2p || s.ext_base) ensure_device_heap();
+    if (s.shm.extra && npes > 1)
+        small_path_setup((char *)s.shm.extra + shm_p2p_region_bytes(), small_shared_bytes(npes));
     if (pe == 0 && (env_flag("VERSION") || env_flag("INFO") || s.debug)) {
         printf("Sandia OpenSHMEM 1.5.3 (MI355X reduction path, libsos_amd)\n");
         if (env_flag("INFO")) print_env();
@@ -641,10 +647,12 @@ void shmem_init(void)
         // node-local shared memory: barriers + peer-to-peer transport counters
         int dummy = 0;
         std::vector<int> all((size_t)size);
-        if (rank == 0 && !s.shm.attach(blob.shm_name, true, rank, p2p_shared_bytes()))
+        // [p2p counters | small-path control words and slots] after the barrier slots
+        const size_t extra = shm_p2p_region_bytes() + small_shared_bytes(size);
+        if (rank == 0 && !s.shm.attach(blob.shm_name, true, rank, extra))
             raise_error("shmem_init: cannot create shared memory %s", blob.shm_name);
         sosboot::hub_allgather(&s.hub, &dummy, sizeof(dummy), all.data());
-        if (rank != 0 && !s.shm.attach(blob.shm_name, false, rank, p2p_shared_bytes()))
+        if (rank != 0 && !s.shm.attach(blob.shm_name, false, rank, extra))
             raise_error("shmem_init: cannot attach shared memory %s", blob.shm_name);
         sosboot::hub_allgather(&s.hub, &dummy, sizeof(dummy), all.data());
         if (rank == 0) shm_unlink(blob.shm_name);
@@ -737,6 +745,7 @@ void shmem_finalize(void)
     s.host_heap = Heap();
     s.dev_heap = Heap();
     p2p_signal_teardown();
+    small_path_teardown();
     s.shm.detach();
     sosboot::hub_close(&s.hub);
     for (auto &kv : s.dev_allocs) (void)hipFree(kv.first);

@@ -176,6 +176,14 @@ void ensure_device_heap();
 
 // Per-pair transport counters living in the shared-memory segment (p2p.cpp).
 size_t p2p_shared_bytes();
+// Small host-resident team reductions through the node shared segment (smallpath.cpp).
+size_t small_shared_bytes(int npes);
+void small_path_setup(void *region, size_t bytes);   // collective (init_common)
+void small_path_teardown();
+bool small_path_takes(int alg, const void *target, const void *source, size_t bytes, const Team &t);
+void small_path_reduce(void *target, const void *source, size_t count, size_t ts, const Team &t,
+                       int op, int dt, const char *fn);
+long small_path_calls();
 void team_word_put(int which, int world_pe, uint64_t v);   // node shm (p2p.cpp)
 uint64_t team_word_get(int which, int world_pe);
 // p2p signalling mode (p2p.cpp): stream-ordered device signals on the registered shm

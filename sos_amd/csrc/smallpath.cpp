@@ -1,0 +1,252 @@
+// smallpath.cpp -- team reductions of small HOST-resident operands without DMA copies.
+//
+// SOS runs a reduction below SHMEM_COLL_SIZE_CROSSOVER as recdbl_sw on host memory
+// (src/shmem_collectives.h:192-195, src/collectives.c:850-984).  On the general path a
+// host operand here costs an H2D copy, the exchange, a D2H copy and their DMA-engine
+// latencies: 52 us per call at P = 2 and 290 us at P = 8 for a few bytes
+// (profiles/r3_small_latency.txt).  This path keeps the bytes where SOS keeps them:
+//   1. each PE copies its source into its slot of the node shared segment (host
+//      memory every PE maps, registered with HIP on every GPU: fine-grained, mapped);
+//   2. host flags (release/acquire) publish the slot to the team;
+//   3. ONE fused fold kernel per PE (sosx_fold, the same kernel the device schedules
+//      use) reads all P slots in place over the host link and writes the PE's result
+//      -- the recdbl_gather evaluation: every PE computes ITS OWN recdbl_sw expression
+//      (the extra-PE folds, then the TREE over the leaves permuted by my_idx; see
+//      plan.cpp build_recdbl_gather), bit for bit, +-0 ties and NaN payloads included;
+//   4. the result lands in `target` directly when it is in the (device-mapped) host
+//      symmetric heap, else in a pinned slot copied out after the stream sync.
+// The arithmetic stays on the GPU; the host only moves the caller's bytes into and out
+// of shared memory, as SOS's puts do.
+//
+// Slot reuse: each PE alternates between two data slots.  A post to receiver r carries
+// a per-pair index k (posted[q][r] = k) and the slot id (ring[q][r][k % 2]); receiver r
+// acknowledges with consumed[r][q] = k after its kernel has read the slot.  Before a PE
+// rewrites a slot it waits until every receiver of that slot's previous post has
+// consumed it, so at most two posts per ordered pair are outstanding and the depth-2
+// ring of slot ids never overwrites an unread entry.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <atomic>
+#include <vector>
+
+#include "plan.h"
+#include "runtime.h"
+#include "sosx.h"
+
+namespace sosrt {
+
+namespace {
+
+constexpr int kMaxPE = 64;
+constexpr size_t kSlotBytes = 64 * 1024;  // the largest operand this path takes
+
+struct alignas(64) PairWord {
+    std::atomic<uint64_t> v;
+    char pad[56];
+};
+
+// Per world PE q: posts to every receiver r, their slot ids, and q's acknowledgements
+// of every sender's posts.  Cache-line separated: a PE spins on words others write.
+struct SmallCtl {
+    PairWord posted[kMaxPE];      // [r]: posts q made for r (count)
+    PairWord consumed[kMaxPE];    // [s]: posts from s that q has read (count)
+    uint32_t ring[kMaxPE][2];     // [r][k % 2]: data slot of q's k-th post for r
+};
+
+struct Small {
+    bool ready = false;          // every PE registered the region (agreed at init)
+    bool registered = false;
+    char *host = nullptr;        // region base (host view)
+    char *dev = nullptr;         // the same bytes, device view
+    size_t bytes = 0;
+    int npes = 0;
+    uint64_t seq = 0;            // my posts (slot = seq % 2)
+    uint64_t posted_to[kMaxPE] = {0};
+    uint64_t seen_from[kMaxPE] = {0};
+    std::vector<std::pair<int, uint64_t>> slot_users[2];  // receivers of each slot's last post
+    void *out = nullptr;         // pinned result slot (hipHostMalloc, device-mapped)
+    void *vscr = nullptr;        // device scratch for the extra-PE folds
+    size_t vscr_bytes = 0;
+    long calls = 0;
+};
+Small g;
+
+size_t ctl_bytes(int npes) { return ((size_t)npes * sizeof(SmallCtl) + 4095) & ~(size_t)4095; }
+
+SmallCtl *ctl(int pe) { return (SmallCtl *)(g.host + (size_t)pe * sizeof(SmallCtl)); }
+
+size_t slot_off(int pe, int sl) { return ctl_bytes(g.npes) + ((size_t)pe * 2 + (size_t)sl) * kSlotBytes; }
+
+double limit_s()
+{
+    const char *e = getenv("SHMEMX_P2P_TIMEOUT");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0 ? v : 300.0;
+}
+
+double now_s()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+void wait_ge(const std::atomic<uint64_t> &w, uint64_t v, const char *what)
+{
+    if (w.load(std::memory_order_acquire) >= v) return;
+    const double t0 = now_s();
+    unsigned spins = 0;
+    while (w.load(std::memory_order_acquire) < v) {
+        __builtin_ia32_pause();
+        if ((++spins & 0xFFFF) == 0 && now_s() - t0 > limit_s())
+            raise_error("small host-resident reduction: timed out after %.0f s waiting for %s",
+                        limit_s(), what);
+    }
+}
+
+}  // namespace
+
+size_t small_shared_bytes(int npes)
+{
+    if (npes < 2 || npes > kMaxPE) return 0;
+    return ctl_bytes(npes) + (size_t)npes * 2 * kSlotBytes;
+}
+
+// Collective (init_common, every PE): register this PE's view of the region with HIP
+// and agree over the bootstrap that every PE could; otherwise the path stays off.
+void small_path_setup(void *region, size_t bytes)
+{
+    State &s = st();
+    g = Small();
+    const char *e = getenv("SHMEMX_SMALL_HOST");
+    const bool want = !(e && !strcmp(e, "0"));
+    if (!s.hub.up || s.n_pes < 2 || s.n_pes > kMaxPE) return;
+    int ok = region != nullptr && bytes >= small_shared_bytes(s.n_pes) && want;
+    void *dptr = nullptr;
+    if (ok) {
+        if (hipHostRegister(region, bytes, kP2PHostRegisterFlags) == hipSuccess) {
+            g.registered = true;
+            ok = hipHostGetDevicePointer(&dptr, region, 0) == hipSuccess && dptr;
+        } else {
+            ok = 0;
+        }
+        if (!ok) (void)hipGetLastError();
+    }
+    if (ok && hipHostMalloc(&g.out, kSlotBytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        g.out = nullptr;
+        ok = 0;
+    }
+    std::vector<int> oks((size_t)s.n_pes);
+    if (sosboot::hub_allgather(&s.hub, &ok, sizeof(ok), oks.data()) != 0)
+        raise_error("shmem_init: small-path agreement failed");
+    for (int v : oks) ok &= v;
+    g.host = (char *)region;
+    g.dev = (char *)dptr;
+    g.bytes = bytes;
+    g.npes = s.n_pes;
+    g.ready = ok != 0;
+    if (!g.ready) small_path_teardown();
+    debug_msg("small host-resident path: %s", g.ready ? "on" : "off");
+}
+
+void small_path_teardown()
+{
+    if (g.registered && g.host) (void)hipHostUnregister(g.host);
+    if (g.out) (void)hipHostFree(g.out);
+    if (g.vscr) (void)hipFree(g.vscr);
+    g = Small();
+}
+
+long small_path_calls() { return g.calls; }
+
+// Does a reduction of `bytes` with these operands over team t take the small path?
+bool small_path_takes(int alg, const void *target, const void *source, size_t bytes, const Team &t)
+{
+    if (!g.ready || bytes == 0 || bytes > kSlotBytes || t.size < 2 || t.size > kMaxPE) return false;
+    if (alg != SOSX_ALG_RECDBL && alg != SOSX_ALG_RECDBL_GATHER) return false;
+    if (sosplan::pow2_floor(t.size) > SOSX_MAX_FOLD) return false;
+    return !is_device_ptr(source) && !is_device_ptr(target);
+}
+
+// recdbl_sw's value for this PE over team t (see the file comment); returns when done.
+void small_path_reduce(void *target, const void *source, size_t count, size_t ts, const Team &t,
+                       int op, int dt, const char *fn)
+{
+    State &s = st();
+    const size_t bytes = count * ts;
+    const int P = t.size, me = t.my_idx, mw = s.my_pe;
+    const int sl = (int)(g.seq++ % 2);
+    // 1. my slot is free once every receiver of its previous post has read it
+    for (const auto &u : g.slot_users[sl]) wait_ge(ctl(u.first)->consumed[mw].v, u.second, "a peer to read a slot");
+    g.slot_users[sl].clear();
+    memcpy(g.host + slot_off(mw, sl), source, bytes);
+    // 2. publish it to the team, then take the peers' posts
+    std::atomic_thread_fence(std::memory_order_release);
+    SmallCtl *mine = ctl(mw);
+    for (int i = 0; i < P; ++i) {
+        if (i == me) continue;
+        const int r = t.world_rank(i);
+        const uint64_t k = ++g.posted_to[r];
+        mine->ring[r][k % 2] = (uint32_t)sl;
+        mine->posted[r].v.store(k, std::memory_order_release);
+        g.slot_users[sl].push_back({r, k});
+    }
+    std::vector<const void *> in((size_t)P);
+    std::vector<int> from((size_t)P, -1);
+    for (int i = 0; i < P; ++i) {
+        const int q = t.world_rank(i);
+        if (i == me) {
+            in[(size_t)i] = g.dev + slot_off(mw, sl);
+            continue;
+        }
+        const uint64_t k = ++g.seen_from[q];
+        wait_ge(ctl(q)->posted[mw].v, k, "a peer's operand");
+        const int qs = (int)ctl(q)->ring[mw][k % 2];
+        in[(size_t)i] = g.dev + slot_off(q, qs);
+        from[(size_t)i] = q;
+    }
+    // 3. the fold: extra PEs first (v[x] = in[x] OP in[x + p2]), then this PE's tree
+    const int p2 = sosplan::pow2_floor(P), nx = P - p2;
+    const int mp = me < p2 ? me : me - p2;
+    if (nx > 0 && g.vscr_bytes < (size_t)nx * kSlotBytes) {
+        if (g.vscr) (void)hipFree(g.vscr);
+        g.vscr = nullptr;
+        hip_check(hipMalloc(&g.vscr, (size_t)nx * kSlotBytes), "hipMalloc(small-path scratch)");
+        g.vscr_bytes = (size_t)nx * kSlotBytes;
+    }
+    int rc = SOSX_OK;
+    for (int x = 0; x < nx && !rc; ++x) {
+        const void *pair[2] = {in[(size_t)x], in[(size_t)(x + p2)]};
+        rc = sosx_fold(op, dt, SOSX_ORDER_LINEAR, (char *)g.vscr + (size_t)x * kSlotBytes, pair, 2,
+                       count, s.stream);
+    }
+    // the result goes straight into the host symmetric heap (device-mapped pinned
+    // memory), else into the pinned result slot
+    const bool direct = s.host_heap.contains(target, bytes);
+    void *out = direct ? target : g.out;
+    if (!rc) {
+        std::vector<const void *> leaves((size_t)p2);
+        for (int y = 0; y < p2; ++y) {
+            const int x = y ^ mp;
+            leaves[(size_t)y] = x < nx ? (const void *)((char *)g.vscr + (size_t)x * kSlotBytes) : in[(size_t)x];
+        }
+        rc = sosx_fold(op, dt, SOSX_ORDER_TREE, out, leaves.data(), p2, count, s.stream);
+    }
+    if (rc) raise_error("%s: small host-resident reduction failed (status %d)", fn, rc);
+    hip_check(hipStreamSynchronize(s.stream), fn);
+    // 4. the peers' slots are read: acknowledge; my result out
+    for (int i = 0; i < P; ++i)
+        if (from[(size_t)i] >= 0)
+            mine->consumed[from[(size_t)i]].v.store(g.seen_from[from[(size_t)i]], std::memory_order_release);
+    if (!direct) memcpy(target, g.out, bytes);
+    g.calls++;
+}
+
+}  // namespace sosrt
+
+extern "C" long sosx_small_path_calls(void) { return sosrt::small_path_calls(); }

@@ -93,8 +93,20 @@ def test_coll_check_rccl_executor(np_):
 
 
 def test_team_management_rccl(np_=4):
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_mgmt_check.py")], timeout=300)
+    """Team management with its reductions on the RCCL executor (their host operands would
+    otherwise take the shared-memory small path, which moves nothing through RCCL)."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_mgmt_check.py")], timeout=300,
+               SHMEMX_SMALL_HOST="0")
     _ok(r, np_)
+
+
+def test_team_management_small_path(np_=4):
+    """The same checks with the default small host-resident path: every reduction of the
+    checker (8-byte host operands) runs through node shared memory, none through RCCL."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_mgmt_check.py")], timeout=300)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK", r.stdout)
+    assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
+    assert "fakerccl error" not in r.stderr, r.stderr[-2000:]
 
 
 def test_api_sweep_rccl(np_=2):

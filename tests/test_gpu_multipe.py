@@ -66,10 +66,25 @@ def test_team_check(np_, signal):
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
                extra_env={"SHMEMX_P2P_SIGNAL": signal})
     # PEs print concurrently, so lines may interleave: count the reports, not lines
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)\)", r.stdout)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+), small-path calls (\d+)\)",
+                    r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _, _ in ok) == list(range(np_)), \
+        r.stdout + r.stderr[-3000:]
+    assert {m for _, m, _ in ok} == {signal}, ok
+    # the host-resident recdbl_sw calls below 64 KiB took the shared-memory path
+    assert all(int(c) > 0 for _, _, c in ok), ok
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_team_check_small_path_off(np_):
+    """SHMEMX_SMALL_HOST=0: the same checks with every host-resident call on the general
+    (staged) path -- both paths give the oracle's bits."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+               extra_env={"SHMEMX_SMALL_HOST": "0"})
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal \w+, small-path calls (\d+)\)", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
         r.stdout + r.stderr[-3000:]
-    assert {m for _, m in ok} == {signal}, ok
+    assert all(int(c) == 0 for _, c in ok), ok
 
 
 @pytest.mark.parametrize("np_,signal", [(2, "host"), (3, "host"), (4, "host"), (8, "host"),
@@ -79,7 +94,7 @@ def test_coll_check(np_, signal):
     moved by the host or by stream-ordered device signals."""
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "coll_check.py")], timeout=900,
                extra_env={"SHMEMX_P2P_SIGNAL": signal})
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)\)", r.stdout)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)[,)]", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
         r.stdout + r.stderr[-3000:]
     assert {m for _, m in ok} == {signal}, ok
@@ -232,7 +247,7 @@ def test_team_check_host_stripes(np_, signal):
         env["GPU_MAX_HW_QUEUES"] = "1"
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
                extra_env=env)
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)\)", r.stdout)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)[,)]", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
         r.stdout + r.stderr[-3000:]
     assert {m for _, m in ok} == {signal}, ok

@@ -2,8 +2,8 @@
 
 Run under tools/oshrun: every PE calls shmem_<T>_<op>_reduce for every schedule
 (auto, ring, recdbl, rechalving, recdbl_direct), several types/ops and sizes, on
-device-heap buffers (shmemx_malloc_device), on plain device buffers and on host
-buffers, in and out of place, over SHMEM_TEAM_WORLD and over a split team.  Each PE
+device-heap buffers (shmemx_malloc_device), on plain device buffers, on pageable host
+buffers and on the host symmetric heap (shmem_malloc), in and out of place, over SHMEM_TEAM_WORLD and over a split team.  Each PE
 checks its own result bit for bit against an on-GPU re-evaluation of the schedule's
 element order over all PEs' regenerated inputs.  Prints one line per PE, exit 0 = OK.
 """
@@ -60,6 +60,8 @@ def main():
     maxn = max(SIZES)
     hsrc = S.shmemx_malloc_device(maxn * 16)
     hdst = S.shmemx_malloc_device(maxn * 16)
+    hh_in = S.lib().shmem_malloc(5003 * 16)       # host symmetric heap (pinned)
+    hh_out = S.lib().shmem_malloc(5003 * 16)
     # an even-PE team (split_strided), when there are at least 3 PEs
     even = ctypes.c_void_p(0)
     if P >= 3:
@@ -80,8 +82,8 @@ def main():
                     continue
                 seed = zlib.crc32(f"{alg}/{tname}/{oname}/{n}".encode())
                 resolved = S.lib().sosx_resolve_alg(L.ALGS[alg], n * es, 16384)
-                for mode in ("heap", "heap_inplace", "device", "host"):
-                    if mode == "host" and n > 5003:
+                for mode in ("heap", "heap_inplace", "device", "host", "hostheap"):
+                    if mode in ("host", "hostheap") and n > 5003:
                         continue
                     L.fill(dt, dist, seed, me, hsrc, n)
                     torch.cuda.synchronize()
@@ -98,11 +100,19 @@ def main():
                         torch.cuda.synchronize()
                         fn(world, t_out.data_ptr(), t_in.data_ptr(), n)
                         out = t_out.data_ptr()
-                    else:
+                    elif mode == "host":
                         h_in = _download(hsrc, n * es)
                         h_out = np.zeros_like(h_in)
                         fn(world, h_out.ctypes.data, h_in.ctypes.data, n)
                         tmp = torch.from_numpy(h_out).cuda()
+                        torch.cuda.synchronize()
+                        out = tmp.data_ptr()
+                    else:
+                        h_in = _download(hsrc, n * es)      # (keep the array alive)
+                        ctypes.memmove(hh_in, h_in.ctypes.data, n * es)
+                        fn(world, hh_out, hh_in, n)
+                        h_out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * es)).from_address(hh_out))
+                        tmp = torch.from_numpy(h_out.copy()).cuda()
                         torch.cuda.synchronize()
                         out = tmp.data_ptr()
                     exp = expected(dt, opid, dist, seed, list(range(P)), me, n, es, resolved, lambda i: i)
@@ -127,12 +137,15 @@ def main():
     S.shmemx_free_device(hsrc)
     if even.value:
         S.lib().shmem_team_destroy(even)
+    S.lib().shmem_free(hh_out)
+    S.lib().shmem_free(hh_in)
     sig = {1: "stream", 0: "host"}.get(L.lib().sosx_p2p_signal_mode(), "none")
+    small = L.lib().sosx_small_path_calls()
     S.shmem_finalize()
     if bad:
         print(f"PE {me}/{P}: {len(bad)} of {checks} checks FAILED: {bad[:6]}", flush=True)
         return 1
-    print(f"PE {me}/{P}: {checks} checks OK (p2p signal {sig})", flush=True)
+    print(f"PE {me}/{P}: {checks} checks OK (p2p signal {sig}, small-path calls {small})", flush=True)
     return 0
 
 

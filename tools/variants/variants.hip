@@ -394,3 +394,43 @@ int sosxv_prefix(int v, void *const *outs, const void *const *ins, int np, size_
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------
+// Host-side completion latency probe (bench only): the cost of learning that one tiny
+// kernel finished, by the ways a library call can wait.  mode 0: hipStreamSynchronize;
+// 1: spin on hipStreamQuery; 2: hipEventRecord + hipEventSynchronize; 3: the kernel
+// stores a flag into pinned host memory (system scope) and the host spins on it.
+// Returns the mean microseconds per launch+wait over `iters`.
+// ---------------------------------------------------------------------------------
+__global__ void k_probe_flag(unsigned *flag, unsigned v)
+{
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+#include <chrono>
+
+extern "C" double sosxv_sync_probe(int mode, int iters, void *stream)
+{
+    hipStream_t st = as_stream(stream);
+    unsigned *flag = nullptr;
+    if (hipHostMalloc((void **)&flag, 64, hipHostMallocDefault) != hipSuccess) return -1.0;
+    *flag = 0;
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1.0;
+    double total = 0;
+    for (int it = -10; it < iters; ++it) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const unsigned v = (unsigned)(it + 11);
+        hipLaunchKernelGGL(k_probe_flag, dim3(1), dim3(64), 0, st, flag, v);
+        if (mode == 0) (void)hipStreamSynchronize(st);
+        else if (mode == 1) { while (hipStreamQuery(st) == hipErrorNotReady) {} }
+        else if (mode == 2) { (void)hipEventRecord(ev, st); (void)hipEventSynchronize(ev); }
+        else { while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != v) __builtin_ia32_pause(); }
+        const auto t1 = std::chrono::steady_clock::now();
+        if (it >= 0) total += std::chrono::duration<double, std::micro>(t1 - t0).count();
+    }
+    (void)hipStreamSynchronize(st);
+    (void)hipEventDestroy(ev);
+    (void)hipHostFree(flag);
+    return total / iters;
+}

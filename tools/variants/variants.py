@@ -58,3 +58,11 @@ def prefix(v, outs, ins, n, stream=None):
     o = (ctypes.c_void_p * k)(*outs)
     i = (ctypes.c_void_p * k)(*ins)
     _check(lib().sosxv_prefix(v, o, i, k, n, stream), "sosxv_prefix")
+
+
+def sync_probe(mode, iters=2000, stream=None):
+    """Mean us per tiny-kernel launch + completion wait (variants.hip sosxv_sync_probe)."""
+    L = lib()
+    L.sosxv_sync_probe.restype = ctypes.c_double
+    L.sosxv_sync_probe.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    return L.sosxv_sync_probe(mode, iters, stream)
