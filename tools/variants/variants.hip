@@ -425,7 +425,17 @@ extern "C" double sosxv_sync_probe(int mode, int iters, void *stream)
         if (mode == 0) (void)hipStreamSynchronize(st);
         else if (mode == 1) { while (hipStreamQuery(st) == hipErrorNotReady) {} }
         else if (mode == 2) { (void)hipEventRecord(ev, st); (void)hipEventSynchronize(ev); }
-        else { while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != v) __builtin_ia32_pause(); }
+        else {  // bounded: a flag that never arrives returns an error after 2 s
+            while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != v) {
+                __builtin_ia32_pause();
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                    (void)hipStreamSynchronize(st);
+                    (void)hipEventDestroy(ev);
+                    (void)hipHostFree(flag);
+                    return -2.0;
+                }
+            }
+        }
         const auto t1 = std::chrono::steady_clock::now();
         if (it >= 0) total += std::chrono::duration<double, std::micro>(t1 - t0).count();
     }
