@@ -138,6 +138,19 @@ int sosx_fold(int op, int dtype, int order, void *out, const void *const *ins, i
 int sosx_prefix(int op, int dtype, void *const *outs, const void *const *ins, int np, int own,
                 size_t count, void *stream);
 
+/*
+ * One PE's recdbl_sw value in one launch (the small host-resident path): leaf y
+ * (y < p2, p2 a power of two <= SOSX_MAX_FOLD) is leaves[y][i], folded first with
+ * extras[y][i] (leaves[y] the left operand) when extras/extras[y] is not null; the
+ * leaves are then reduced by the recdbl_sw tree (SOSX_ORDER_TREE).  Completion is
+ * signalled in memory, not by the stream: workgroup b (b < ceil(count / 256)) stores
+ * `seq` into flags[b] (pinned host memory) after its results are visible system-wide.
+ */
+#define SOSX_SMALL_FOLD_MAX 65536
+int sosx_small_fold(int op, int dtype, void *out, const void *const *leaves,
+                    const void *const *extras, int p2, size_t count, uint32_t *flags,
+                    uint32_t seq, void *stream);
+
 /* Fill `count` elements of device buffer dst with the synthetic input of PE `pe`,
  * element indices [index0, index0 + count).  Bit-identical to the CPU generator
  * (tests/ and bench.py use oracle/sos_oracle.c's oracle_fill). */
@@ -151,6 +164,11 @@ int sosx_count_mismatch(const void *a, const void *b, size_t count, size_t elem_
 
 /* Synchronous copy between any host/device addresses (hipMemcpyDefault semantics). */
 int sosx_memcpy(void *dst, const void *src, size_t bytes, void *stream);
+
+/* Store `value` into *word (pinned host memory, device-visible) after all earlier work
+ * on `stream` has finished: a completion mark the host polls instead of synchronising
+ * the stream. */
+int sosx_stream_mark(uint32_t *word, uint32_t value, void *stream);
 
 /* Multi-segment copy in one launch (peer-to-peer transport gathers). */
 int sosx_gather(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,

@@ -61,6 +61,7 @@ struct Prof {
     }
     void collect()
     {
+        (void)hipStreamSynchronize(sosrt::st().stream);  // every event of the call complete
         for (size_t i = 0; i < nf; ++i) {
             float ms = 0;
             if (hipEventElapsedTime(&ms, fold_ev[i].first, fold_ev[i].second) == hipSuccess) fold_ms += ms;
@@ -292,9 +293,12 @@ void execute_p2p(const Plan &p, const Team &t, int alg, size_t count, size_t ts,
     if (g_prof.on) g_prof.ncall++;
     int rc = p2p_exec(p, t, alg, count, ts, pb, op, dt, s.stream);
     if (rc) raise_error("%s: %s", fn, status_text(rc));
-    if (!direct && p.writes_dst)
+    // p2p_exec returned with the stream drained; a staged result still has to come out
+    // (its target may be pageable memory: a full stream synchronisation)
+    if (!direct && p.writes_dst) {
         hip_check(hipMemcpyAsync(target, s.sym_stage, bytes, hipMemcpyDefault, s.stream), "stage out");
-    hip_check(hipStreamSynchronize(s.stream), fn);
+        hip_check(hipStreamSynchronize(s.stream), fn);
+    }
     if (g_prof.on) g_prof.collect();
 }
 
@@ -517,9 +521,12 @@ void execute(int alg, void *target, const void *source, size_t count, size_t ts,
         if (ncclAllReduce(dsrc, ddst, count, ar_ty, ar_op, s.comm, s.stream) != ncclSuccess)
             raise_error("%s: %s", fn, status_text(SOSX_ERR_RCCL));
         if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, true), s.stream);
-        if (!dev_dst)
+        if (!dev_dst) {
             hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
-        hip_check(hipStreamSynchronize(s.stream), fn);
+            hip_check(hipStreamSynchronize(s.stream), fn);
+        } else {
+            hip_check(stream_wait(s.stream), fn);
+        }
         if (g_prof.on) g_prof.collect();
         return;
     }
@@ -531,9 +538,12 @@ void execute(int alg, void *target, const void *source, size_t count, size_t ts,
     if (g_prof.on) g_prof.ncall++;
     rc = exec_rccl(p, t, b, op, dt, s.stream);
     if (rc) raise_error("%s: %s", fn, status_text(rc));
-    if (!dev_dst && p.writes_dst)
+    if (!dev_dst && p.writes_dst) {  // the target may be pageable: a full synchronisation
         hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
-    hip_check(hipStreamSynchronize(s.stream), fn);
+        hip_check(hipStreamSynchronize(s.stream), fn);
+    } else {
+        hip_check(stream_wait(s.stream), fn);
+    }
     if (g_prof.on) g_prof.collect();
 }
 

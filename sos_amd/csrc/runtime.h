@@ -138,6 +138,13 @@ void debug_msg(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 
 void check_initialized(const char *fn);
 void hip_check(hipError_t e, const char *what);
+
+// Wait until all work queued on `st` has finished, as hipStreamSynchronize does, by
+// polling a completion mark in pinned host memory (sosx_stream_mark): about 5 us less
+// per wait (profiles/r3_sync_probe.json).  Errors as hipStreamSynchronize reports them.
+// Not for streams with pending copies to PAGEABLE host memory (the runtime finishes
+// those on the host).
+hipError_t stream_wait(hipStream_t st);
 void nccl_check(ncclResult_t r, const char *what);
 
 // Device workspaces (grown, never shrunk).

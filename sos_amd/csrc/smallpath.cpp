@@ -8,13 +8,15 @@
 //   1. each PE copies its source into its slot of the node shared segment (host
 //      memory every PE maps, registered with HIP on every GPU: fine-grained, mapped);
 //   2. host flags (release/acquire) publish the slot to the team;
-//   3. ONE fused fold kernel per PE (sosx_fold, the same kernel the device schedules
-//      use) reads all P slots in place over the host link and writes the PE's result
-//      -- the recdbl_gather evaluation: every PE computes ITS OWN recdbl_sw expression
-//      (the extra-PE folds, then the TREE over the leaves permuted by my_idx; see
-//      plan.cpp build_recdbl_gather), bit for bit, +-0 ties and NaN payloads included;
+//   3. ONE kernel per PE (sosx_small_fold) reads all P slots in place over the host
+//      link and writes the PE's result -- the recdbl_gather evaluation: every PE
+//      computes ITS OWN recdbl_sw expression (the extra-PE folds, then the TREE over the
+//      leaves permuted by my_idx; see plan.cpp build_recdbl_gather), bit for bit, +-0
+//      ties and NaN payloads included;
 //   4. the result lands in `target` directly when it is in the (device-mapped) host
-//      symmetric heap, else in a pinned slot copied out after the stream sync.
+//      symmetric heap, else in a pinned slot copied out; the host learns that the kernel
+//      finished from per-workgroup completion words in pinned memory, not from a
+//      stream synchronisation (about 5 us less per call).
 // The arithmetic stays on the GPU; the host only moves the caller's bytes into and out
 // of shared memory, as SOS's puts do.
 //
@@ -43,6 +45,7 @@ namespace {
 
 constexpr int kMaxPE = 64;
 constexpr size_t kSlotBytes = 64 * 1024;  // the largest operand this path takes
+constexpr size_t kFlagWords = kSlotBytes / 256;  // one per workgroup of a 1-byte-type fold
 
 struct alignas(64) PairWord {
     std::atomic<uint64_t> v;
@@ -69,8 +72,8 @@ struct Small {
     uint64_t seen_from[kMaxPE] = {0};
     std::vector<std::pair<int, uint64_t>> slot_users[2];  // receivers of each slot's last post
     void *out = nullptr;         // pinned result slot (hipHostMalloc, device-mapped)
-    void *vscr = nullptr;        // device scratch for the extra-PE folds
-    size_t vscr_bytes = 0;
+    uint32_t *flags = nullptr;   // per-workgroup completion words (pinned, coherent)
+    uint32_t fseq = 0;           // the value the current launch's workgroups store
     long calls = 0;
 };
 Small g;
@@ -108,6 +111,36 @@ void wait_ge(const std::atomic<uint64_t> &w, uint64_t v, const char *what)
     }
 }
 
+// Wait until workgroups [0, nb) of the small fold stored `seq`.  The host polls pinned
+// memory instead of synchronising the stream (a launch + hipStreamSynchronize costs
+// ~12 us, a launch + flag poll ~6.6 us: profiles/r3_sync_probe.json).  Every 4096 polls
+// the stream is queried: an error, or a drained stream whose flags are still missing,
+// ends the job with a message, as does SHMEMX_P2P_TIMEOUT.
+void wait_flags(int nb, uint32_t seq, const char *fn)
+{
+    const double t0 = now_s();
+    unsigned spins = 0;
+    for (int b = 0; b < nb;) {
+        if (__atomic_load_n(g.flags + b, __ATOMIC_ACQUIRE) == seq) {
+            ++b;
+            continue;
+        }
+        __builtin_ia32_pause();
+        if ((++spins & 0xFFF) != 0) continue;
+        const hipError_t e = hipStreamQuery(st().stream);
+        if (e == hipSuccess) {  // drained: every flag must be visible by now
+            for (int k = b; k < nb; ++k)
+                if (__atomic_load_n(g.flags + k, __ATOMIC_ACQUIRE) != seq)
+                    raise_error("%s: small host-resident reduction: workgroup %d of %d did not "
+                                "signal completion", fn, k, nb);
+            return;
+        }
+        if (e != hipErrorNotReady) hip_check(e, fn);
+        if (now_s() - t0 > limit_s())
+            raise_error("%s: small host-resident reduction: timed out after %.0f s", fn, limit_s());
+    }
+}
+
 }  // namespace
 
 size_t small_shared_bytes(int npes)
@@ -141,6 +174,12 @@ void small_path_setup(void *region, size_t bytes)
         g.out = nullptr;
         ok = 0;
     }
+    if (ok && hipHostMalloc((void **)&g.flags, kFlagWords * sizeof(uint32_t), hipHostMallocCoherent) != hipSuccess) {
+        (void)hipGetLastError();
+        g.flags = nullptr;
+        ok = 0;
+    }
+    if (g.flags) memset(g.flags, 0, kFlagWords * sizeof(uint32_t));
     std::vector<int> oks((size_t)s.n_pes);
     if (sosboot::hub_allgather(&s.hub, &ok, sizeof(ok), oks.data()) != 0)
         raise_error("shmem_init: small-path agreement failed");
@@ -158,7 +197,7 @@ void small_path_teardown()
 {
     if (g.registered && g.host) (void)hipHostUnregister(g.host);
     if (g.out) (void)hipHostFree(g.out);
-    if (g.vscr) (void)hipFree(g.vscr);
+    if (g.flags) (void)hipHostFree(g.flags);
     g = Small();
 }
 
@@ -210,36 +249,27 @@ void small_path_reduce(void *target, const void *source, size_t count, size_t ts
         in[(size_t)i] = g.dev + slot_off(q, qs);
         from[(size_t)i] = q;
     }
-    // 3. the fold: extra PEs first (v[x] = in[x] OP in[x + p2]), then this PE's tree
+    // 3. one launch: this PE's recdbl_sw tree over the leaves w[y] = v[y ^ mp], where
+    //    v[x] = in[x] OP in[x + p2] for the extra PEs (x < P - p2), else in[x]
     const int p2 = sosplan::pow2_floor(P), nx = P - p2;
     const int mp = me < p2 ? me : me - p2;
-    if (nx > 0 && g.vscr_bytes < (size_t)nx * kSlotBytes) {
-        if (g.vscr) (void)hipFree(g.vscr);
-        g.vscr = nullptr;
-        hip_check(hipMalloc(&g.vscr, (size_t)nx * kSlotBytes), "hipMalloc(small-path scratch)");
-        g.vscr_bytes = (size_t)nx * kSlotBytes;
-    }
-    int rc = SOSX_OK;
-    for (int x = 0; x < nx && !rc; ++x) {
-        const void *pair[2] = {in[(size_t)x], in[(size_t)(x + p2)]};
-        rc = sosx_fold(op, dt, SOSX_ORDER_LINEAR, (char *)g.vscr + (size_t)x * kSlotBytes, pair, 2,
-                       count, s.stream);
+    std::vector<const void *> leaves((size_t)p2), extras((size_t)p2);
+    for (int y = 0; y < p2; ++y) {
+        const int x = y ^ mp;
+        leaves[(size_t)y] = in[(size_t)x];
+        extras[(size_t)y] = x < nx ? in[(size_t)(x + p2)] : nullptr;
     }
     // the result goes straight into the host symmetric heap (device-mapped pinned
     // memory), else into the pinned result slot
     const bool direct = s.host_heap.contains(target, bytes);
     void *out = direct ? target : g.out;
-    if (!rc) {
-        std::vector<const void *> leaves((size_t)p2);
-        for (int y = 0; y < p2; ++y) {
-            const int x = y ^ mp;
-            leaves[(size_t)y] = x < nx ? (const void *)((char *)g.vscr + (size_t)x * kSlotBytes) : in[(size_t)x];
-        }
-        rc = sosx_fold(op, dt, SOSX_ORDER_TREE, out, leaves.data(), p2, count, s.stream);
-    }
+    if (++g.fseq == 0) g.fseq = 1;
+    const int rc = sosx_small_fold(op, dt, out, leaves.data(), extras.data(), p2, count, g.flags, g.fseq,
+                                   s.stream);
     if (rc) raise_error("%s: small host-resident reduction failed (status %d)", fn, rc);
-    hip_check(hipStreamSynchronize(s.stream), fn);
-    // 4. the peers' slots are read: acknowledge; my result out
+    // 4. completion from the workgroups' flags (no stream synchronisation); then the
+    //    peers' slots are read: acknowledge; my result out
+    wait_flags((int)((count + 255) / 256), g.fseq, fn);
     for (int i = 0; i < P; ++i)
         if (from[(size_t)i] >= 0)
             mine->consumed[from[(size_t)i]].v.store(g.seen_from[from[(size_t)i]], std::memory_order_release);

@@ -209,3 +209,18 @@ def test_p2p_mapping_flags():
     for bad in ("hipExtHostRegisterCoarseGrained", "hipHostRegisterIoMemory", "hipExtHostRegisterUncached"):
         assert not reg.value & _hip_define(bad), bad
     assert ipc.value == _hip_define("hipIpcMemLazyEnablePeerAccess")
+
+
+def test_small_fold_rejects_bad_args():
+    """sosx_small_fold validates before any device work (CPU)."""
+    import ctypes
+    from sos_amd import _lib
+    L = _lib.lib()
+    one = (ctypes.c_void_p * 1)(1)
+    flags = 1
+    assert L.sosx_small_fold(5, 23, None, one, None, 3, 1, flags, 1, None) == -3       # p2 not pow2
+    assert L.sosx_small_fold(5, 23, None, one, None, 1, 65537, flags, 1, None) == -3   # too long
+    assert L.sosx_small_fold(5, 23, None, one, None, 1, 1, None, 1, None) == -3        # no flags
+    assert L.sosx_small_fold(0, 23, None, one, None, 1, 1, flags, 1, None) == -2       # and on float
+    assert L.sosx_small_fold(5, 0, None, one, None, 1, 1, flags, 1, None) == -1        # SIGNED_BYTE
+    assert L.sosx_small_fold(5, 23, None, one, None, 1, 0, flags, 1, None) == 0        # count 0

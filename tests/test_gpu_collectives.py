@@ -217,3 +217,55 @@ def test_gather_kernel(torch_cuda, case):
     for (s, so, n), (d, do, _) in zip(srcs, dsts):
         assert torch.equal(d[do:do + n], s[so:so + n])
         assert bool((d[:do] == 0xA5).all()) and bool((d[do + n:] == 0xA5).all())
+
+
+def _perspective_inputs(dt, P, n, seed):
+    """Inputs whose recdbl_sw value depends on the PE: fp +-0 ties and NaNs with a
+    distinct payload per PE (x86 keeps the first NaN operand), next to ordinary values."""
+    srcs = [src_of(dt, seed, p, n) for p in range(P)]
+    if dt in (23, 24):
+        ity = np.uint32 if dt == 23 else np.uint64
+        nan0 = ity(0x7FC00000) if dt == 23 else ity(0x7FF8000000000000)
+        for p in range(P):
+            s = srcs[p]
+            s[0] = -0.0 if p % 2 else 0.0
+            s.view(ity)[min(1, n - 1)] = nan0 | ity(p + 1)
+    return srcs
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 7, 8, 12, 16])
+@pytest.mark.parametrize("dt,op", [(23, 5), (24, 4), (23, 3), (4, 3), (27, 6), (25, 5), (1, 6)])
+def test_small_fold_kernel(torch_cuda, P, dt, op):
+    """sosx_small_fold (the small host-resident path's one launch): operands, result and
+    completion words all in pinned host memory, every PE's own recdbl_sw value (oracle
+    recdbl, per PE: +-0 ties and NaN payloads included), and every workgroup's
+    completion word set to the call's sequence number."""
+    import ctypes
+    torch = torch_cuda
+    L = _lib.lib()
+    p2 = 1 << (P.bit_length() - 1)
+    nx = P - p2
+    flags = torch.zeros(256, dtype=torch.int32, pin_memory=True)
+    seq = 0
+    for n in (1, 255, 257, 4095):
+        srcs = _perspective_inputs(dt, P, n, seed=n + P)
+        ref = O.recdbl(op, dt, srcs)
+        host = [torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory() for a in srcs]
+        out = torch.zeros(srcs[0].nbytes, dtype=torch.uint8, pin_memory=True)
+        for me in sorted({0, P // 2, P - 1}):
+            mp = me if me < p2 else me - p2
+            leaves = [host[y ^ mp].data_ptr() for y in range(p2)]
+            extras = [host[(y ^ mp) + p2].data_ptr() if (y ^ mp) < nx else None for y in range(p2)]
+            seq += 1
+            out.fill_(0xA5)
+            rc = L.sosx_small_fold(op, dt, ctypes.c_void_p(out.data_ptr()),
+                                   (ctypes.c_void_p * p2)(*leaves), (ctypes.c_void_p * p2)(*extras),
+                                   p2, ctypes.c_size_t(n), ctypes.c_void_p(flags.data_ptr()),
+                                   ctypes.c_uint32(seq), None)
+            assert rc == 0
+            torch.cuda.synchronize()
+            nb = (n + 255) // 256
+            assert bool((flags[:nb] == seq).all()), (n, me, flags[:nb].tolist())
+            got = np.frombuffer(out.numpy().tobytes(), srcs[0].dtype)
+            assert np.array_equal(bits(got), bits(ref[me])), (P, dt, op, n, me)
+

@@ -14,12 +14,18 @@ def main():
     torch.cuda.set_device(0)
     s = torch.cuda.Stream()
     names = ["hipStreamSynchronize", "hipStreamQuery spin", "hipEventSynchronize",
-             "host spin on a flag the kernel stores"]
+             "host spin on a flag the kernel stores",
+             "one hipStreamQuery, then host spin on the flag",
+             "hipStreamQuery of an idle stream alone (no launch)"]
     out = {}
     for _ in range(2):
         for m, name in enumerate(names):
             out[name] = round(V.sync_probe(m, 2000, s.cuda_stream), 2)
-    print(json.dumps({"us_per_launch_and_wait": out}))
+    svc = {}
+    for n in (1, 64, 1024, 4096):
+        svc[n] = round(V.service_probe(n, 2000, s.cuda_stream), 2)
+    print(json.dumps({"us_per_launch_and_wait": out,
+                      "persistent_kernel_round_trip_us_by_n": svc}))
 
 
 if __name__ == "__main__":

@@ -66,3 +66,12 @@ def sync_probe(mode, iters=2000, stream=None):
     L.sosxv_sync_probe.restype = ctypes.c_double
     L.sosxv_sync_probe.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     return L.sosxv_sync_probe(mode, iters, stream)
+
+
+def service_probe(n, iters=2000, stream=None):
+    """Mean us per host->GPU->host round trip of a persistent one-workgroup kernel that
+    adds two n-float pinned slots per request (variants.hip sosxv_service_probe)."""
+    L = lib()
+    L.sosxv_service_probe.restype = ctypes.c_double
+    L.sosxv_service_probe.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    return L.sosxv_service_probe(n, iters, stream)
