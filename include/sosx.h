@@ -143,13 +143,25 @@ int sosx_prefix(int op, int dtype, void *const *outs, const void *const *ins, in
  * (y < p2, p2 a power of two <= SOSX_MAX_FOLD) is leaves[y][i], folded first with
  * extras[y][i] (leaves[y] the left operand) when extras/extras[y] is not null; the
  * leaves are then reduced by the recdbl_sw tree (SOSX_ORDER_TREE).  Completion is
- * signalled in memory, not by the stream: workgroup b (b < ceil(count / 256)) stores
- * `seq` into flags[b] (pinned host memory) after its results are visible system-wide.
+ * signalled in memory, not by the stream: workgroup b (b < *nblocks) stores `seq` into
+ * flags[b] (pinned host memory) after its results are visible system-wide; flags must
+ * hold count / 256 + 8 words.  count <= SOSX_SMALL_FOLD_MAX.
  */
-#define SOSX_SMALL_FOLD_MAX 65536
+#define SOSX_SMALL_FOLD_MAX (1 << 20)
 int sosx_small_fold(int op, int dtype, void *out, const void *const *leaves,
                     const void *const *extras, int p2, size_t count, uint32_t *flags,
-                    uint32_t seq, void *stream);
+                    uint32_t seq, int *nblocks, void *stream);
+
+/*
+ * Every element's SOS ring value in one launch (the small host-resident path above the
+ * crossover): element i of ring chunk c (src/collectives.c:697-709) is the LINEAR fold
+ * ((ins[c] OP ins[c+1]) OP ...) OP ins[c-1] of the np (2..8) team operands, the value
+ * SOS's ring reduce-scatter + allgather leaves in every PE's target.  Completion words
+ * as sosx_small_fold; *nblocks receives how many workgroups store one (<= count / 256
+ * + np).  count <= SOSX_SMALL_FOLD_MAX.
+ */
+int sosx_small_ring(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
+                    uint32_t *flags, uint32_t seq, int *nblocks, void *stream);
 
 /* Fill `count` elements of device buffer dst with the synthetic input of PE `pe`,
  * element indices [index0, index0 + count).  Bit-identical to the CPU generator

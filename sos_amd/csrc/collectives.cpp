@@ -572,10 +572,11 @@ void op_to_all(void *target, const void *source, size_t count, size_t ts, const 
         alg = SOSX_ALG_RECHALVING;
     if (alg == SOSX_ALG_RECDBL_GATHER && sosplan::pow2_floor(t.size) > SOSX_MAX_FOLD)
         alg = SOSX_ALG_RECDBL;
-    // recdbl_sw on small host-resident operands: through the node shared segment, one
-    // fold kernel reading every PE's operand in place (smallpath.cpp), no DMA copies
+    // small host-resident operands (recdbl_sw below the crossover, the ring above it):
+    // through the node shared segment, one kernel reading every PE's operand in place
+    // (smallpath.cpp), no DMA copies
     if (!s.rccl_allreduce && small_path_takes(alg, target, source, bytes, t)) {
-        small_path_reduce(target, source, count, ts, t, op, dt, fn);
+        small_path_reduce(alg, target, source, count, ts, t, op, dt, fn);
         return;
     }
     execute(alg, target, source, count, ts, t, op, dt, fn, true);

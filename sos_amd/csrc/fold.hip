@@ -90,100 +90,16 @@ __global__ __launch_bounds__(kThreads) void k_prefix_dyn(PrefixPtrs p, int np, i
         prefix_elem_dyn<T, OP>(p, np, own, i);
 }
 
-// ---------------------------------------------------------------------------------
-// The small host-resident path's whole recdbl_sw evaluation for one PE in ONE launch
-// (smallpath.cpp): leaf y of the tree is in[y ^ me'] folded with its extra PE's operand
-// (in[x] OP in[x + p2], src/collectives.c:905-926) when it has one, then the recdbl_sw
-// tree over the P2 leaves (fold_elem TREE).  One element per lane, every operand loaded
-// before the first op: the operands sit in host memory, so the loads' latency, not
-// bandwidth, bounds the call.  Completion is signalled without a stream synchronisation:
-// every lane fences its store at system scope, then the workgroup stores `seq` into its
-// own completion word in pinned host memory, which the host polls.
-// ---------------------------------------------------------------------------------
-struct SmallFoldArgs {
-    const void *leaf[SOSX_MAX_FOLD];
-    const void *extra[SOSX_MAX_FOLD];  // null: the leaf has no extra PE
-    uint32_t *flags;                   // one word per workgroup
-    uint32_t seq;
-    int p2;                            // runtime leaf count (P2 == 0 instantiation)
-};
-
-template <class T, class OP, int P2>
-__global__ __launch_bounds__(kThreads) void k_small_fold(T *out, SmallFoldArgs a, size_t n)
-{
-    const size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
-    if (i < n) {
-        if constexpr (P2 > 0) {
-            T v[P2], x[P2];
-#pragma unroll
-            for (int y = 0; y < P2; ++y) {
-                v[y] = ((const T *)a.leaf[y])[i];
-                if (a.extra[y]) x[y] = ((const T *)a.extra[y])[i];
-            }
-#pragma unroll
-            for (int y = 0; y < P2; ++y)
-                if (a.extra[y]) v[y] = OP::f(v[y], x[y]);
-            out[i] = fold_elem<T, OP, P2, SOSX_ORDER_TREE>(v);
-        } else {  // 16..64 leaves (several PEs per GPU): the binary-counter walk of k_fold_dyn
-            T val[8];
-            int height[8];
-            int top = 0;
-            for (int y = 0; y < a.p2; ++y) {
-                T leaf = ((const T *)a.leaf[y])[i];
-                if (a.extra[y]) leaf = OP::f(leaf, ((const T *)a.extra[y])[i]);
-                val[top] = leaf;
-                height[top] = 0;
-                ++top;
-                while (top >= 2 && height[top - 1] == height[top - 2]) {
-                    val[top - 2] = OP::f(val[top - 2], val[top - 1]);
-                    height[top - 2]++;
-                    --top;
-                }
-            }
-            out[i] = val[0];
-        }
-    }
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_store(a.flags + blockIdx.x, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 }  // namespace sos
 
 using namespace sos;
 
 namespace {
 
-struct SmallFoldFn {
-    template <class T, class OP>
-    static int run(void *out, const SmallFoldArgs *a, size_t n, hipStream_t st)
-    {
-        const unsigned blocks = (unsigned)((n + kThreads - 1) / kThreads);
-        switch (a->p2) {
-#define SOS_SMALL(P2)                                                                         \
-    case P2:                                                                                  \
-        hipLaunchKernelGGL((k_small_fold<T, OP, P2>), dim3(blocks), dim3(kThreads), 0, st, (T *)out, \
-                           *a, n);                                                            \
-        break;
-            SOS_SMALL(1)
-            SOS_SMALL(2)
-            SOS_SMALL(4)
-            SOS_SMALL(8)
-#undef SOS_SMALL
-            default:
-                hipLaunchKernelGGL((k_small_fold<T, OP, 0>), dim3(blocks), dim3(kThreads), 0, st, (T *)out,
-                                   *a, n);
-        }
-        return hip_ok(hipGetLastError());
-    }
-};
-
 // Inputs of at most this many bytes each are folded one element per lane: the grid then
-// has n/256 workgroups instead of n/(256*U*V), so a small fold whose inputs sit in host
-// memory (the small host-resident path, smallpath.cpp) or behind xGMI has many
-// workgroups' loads in flight at once instead of one workgroup's; latency, not
-// bandwidth, bounds these calls.
+// has n/256 workgroups instead of n/(256*U*V), so a small fold whose inputs sit behind
+// xGMI (the p2p transport's folds read peers in place) has many workgroups' loads in
+// flight at once instead of one workgroup's; latency, not bandwidth, bounds these calls.
 constexpr size_t kSpreadBytes = 64 * 1024;
 
 template <class T, class OP, int NP, int ORDER>
@@ -318,32 +234,6 @@ int sosx_fold(int op, int dtype, int order, void *out, const void *const *ins, i
     memset(&fp, 0, sizeof(fp));
     for (int k = 0; k < nin; ++k) fp.p[k] = ins[k];
     return dispatch<FoldFn>(op, dtype, order, out, &fp, nin, count, as_stream(stream));
-}
-
-// One PE's recdbl_sw value over p2 leaves (leaves[y], each folded first with extras[y]
-// when that is not null), written to `out`; workgroup b then stores `seq` into flags[b]
-// (b < ceil(count / 256), flags in pinned host memory).  count <= SOSX_SMALL_FOLD_MAX.
-int sosx_small_fold(int op, int dtype, void *out, const void *const *leaves,
-                    const void *const *extras, int p2, size_t count, uint32_t *flags, uint32_t seq,
-                    void *stream)
-{
-    if (p2 < 1 || p2 > SOSX_MAX_FOLD || (p2 & (p2 - 1)) || count > SOSX_SMALL_FOLD_MAX || !flags)
-        return SOSX_ERR_ARG;
-    int rc = sos_check_op(op, dtype);
-    if (rc) return rc;
-    if (count == 0) return SOSX_OK;
-    if (!out || !leaves) return SOSX_ERR_ARG;
-    SmallFoldArgs a;
-    memset(&a, 0, sizeof(a));
-    for (int y = 0; y < p2; ++y) {
-        if (!leaves[y]) return SOSX_ERR_ARG;
-        a.leaf[y] = leaves[y];
-        a.extra[y] = extras ? extras[y] : nullptr;
-    }
-    a.flags = flags;
-    a.seq = seq;
-    a.p2 = p2;
-    return dispatch<SmallFoldFn>(op, dtype, out, (const SmallFoldArgs *)&a, count, as_stream(stream));
 }
 
 }  // extern "C"

@@ -194,6 +194,8 @@ static size_t atol_scaled(const char *s, size_t dflt)
     return (size_t)v;
 }
 
+size_t env_size(const char *name, size_t dflt) { return atol_scaled(getenv(name), dflt); }
+
 static const char *getenv2(const char *name)
 {
     // SOS accepts SHMEM_<X> and SMA_<X> (src/shmem_env.c:90-117)
@@ -251,6 +253,10 @@ static const EnvDef kEnv[] = {
     {"SHMEMX_P2P_SIGNAL", "string", "stream on one GPU, host across GPUs", "device",
      "p2p round signalling: stream (device) or host"},
     {"SHMEMX_P2P_TIMEOUT", "long", "300", "device", "Seconds before a p2p wait ends the job"},
+    {"SHMEMX_SMALL_HOST", "bool", "true", "device",
+     "Host-resident team reductions of small operands through node shared memory"},
+    {"SHMEMX_SMALL_HOST_BYTES", "size", "1048576", "device",
+     "Largest operand of that path (its slots: at most 32 MiB over all PEs)"},
 };
 
 static void print_env()

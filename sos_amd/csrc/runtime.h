@@ -137,6 +137,8 @@ void warn(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 void debug_msg(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 
 void check_initialized(const char *fn);
+// A size from the environment (K/M/G suffixes, as SOS's size parameters), or `dflt`.
+size_t env_size(const char *name, size_t dflt);
 void hip_check(hipError_t e, const char *what);
 
 // Wait until all work queued on `st` has finished, as hipStreamSynchronize does, by
@@ -188,8 +190,8 @@ size_t small_shared_bytes(int npes);
 void small_path_setup(void *region, size_t bytes);   // collective (init_common)
 void small_path_teardown();
 bool small_path_takes(int alg, const void *target, const void *source, size_t bytes, const Team &t);
-void small_path_reduce(void *target, const void *source, size_t count, size_t ts, const Team &t,
-                       int op, int dt, const char *fn);
+void small_path_reduce(int alg, void *target, const void *source, size_t count, size_t ts,
+                       const Team &t, int op, int dt, const char *fn);
 long small_path_calls();
 void team_word_put(int which, int world_pe, uint64_t v);   // node shm (p2p.cpp)
 uint64_t team_word_get(int which, int world_pe);

@@ -1,0 +1,339 @@
+// small.hip -- the kernels of the small host-resident path (smallpath.cpp).
+//
+// Below a few MiB per team, a reduction whose operands live in host memory (SOS's
+// symmetric heap) is latency bound: staging it through HBM costs two DMA round trips and
+// the exchange's rounds.  The small path puts every PE's operand in a slot of node shared
+// memory that every GPU maps, and ONE kernel per PE reads all P slots over the host link
+// and writes that PE's result:
+//   k_small_fold : recdbl_sw (AUTO below SHMEM_COLL_SIZE_CROSSOVER), this PE's own tree;
+//   k_small_ring : the ring (AUTO above it), every chunk folded from its owner.
+// Each lane handles one 16-B vector of every operand when the operands are 16-B aligned
+// (the slots are), so a wave moves 1 KiB per load over PCIe instead of 256 B; the few
+// elements that do not fill a vector go one per lane.  Completion is signalled without a
+// stream synchronisation: every lane fences its stores at system scope and each
+// workgroup then stores the call's sequence number into its own word of pinned host
+// memory, which the host polls.
+#include "fold_kernels.h"
+
+namespace sos {
+
+// recdbl_sw from one PE's perspective: leaf y is leaf[y] OP extra[y] (the extra PE folded
+// in first, src/collectives.c:905-926) or leaf[y] alone; the leaves are then reduced by
+// the butterfly's tree (:932-963, fold_elem TREE).  P2 = 0: a runtime leaf count of 16..64
+// (several PEs per GPU), walked with the binary-counter stack of k_fold_dyn.
+struct SmallFoldArgs {
+    const void *leaf[SOSX_MAX_FOLD];
+    const void *extra[SOSX_MAX_FOLD];  // null: the leaf has no extra PE
+    uint32_t *flags;                   // one word per workgroup
+    uint32_t seq;
+    int p2;
+    int vec_out;                       // out is 16-B aligned: vector stores
+};
+
+template <class T, class OP, int P2>
+__device__ __forceinline__ T small_tree_elem(const SmallFoldArgs &a, size_t i)
+{
+    if constexpr (P2 > 0) {
+        T v[P2], x[P2];
+#pragma unroll
+        for (int y = 0; y < P2; ++y) {
+            v[y] = ((const T *)a.leaf[y])[i];
+            if (a.extra[y]) x[y] = ((const T *)a.extra[y])[i];
+        }
+#pragma unroll
+        for (int y = 0; y < P2; ++y)
+            if (a.extra[y]) v[y] = OP::f(v[y], x[y]);
+        return fold_elem<T, OP, P2, SOSX_ORDER_TREE>(v);
+    } else {
+        T val[8];
+        int height[8];
+        int top = 0;
+        for (int y = 0; y < a.p2; ++y) {
+            T leaf = ((const T *)a.leaf[y])[i];
+            if (a.extra[y]) leaf = OP::f(leaf, ((const T *)a.extra[y])[i]);
+            val[top] = leaf;
+            height[top] = 0;
+            ++top;
+            while (top >= 2 && height[top - 1] == height[top - 2]) {
+                val[top - 2] = OP::f(val[top - 2], val[top - 1]);
+                height[top - 2]++;
+                --top;
+            }
+        }
+        return val[0];
+    }
+}
+
+__device__ __forceinline__ void signal_done(uint32_t *flags, uint32_t seq)
+{
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <class T>
+__device__ __forceinline__ void store_pack(T *out, size_t i0, const Pack<T> &r, bool vec)
+{
+    if (vec) {
+        *reinterpret_cast<u32x4 *>(out + i0) = __builtin_bit_cast(u32x4, r);
+    } else {
+#pragma unroll
+        for (int j = 0; j < Pack<T>::N; ++j) out[i0 + j] = r.e[j];
+    }
+}
+
+// VEC: lane L handles elements [L*V, L*V + V) as 16-B vectors (every leaf/extra 16-B
+// aligned); the last, partial vector goes element by element.  Otherwise one element per
+// lane.
+template <class T, class OP, int P2, bool VEC>
+__global__ __launch_bounds__(kThreads) void k_small_fold(T *out, SmallFoldArgs a, size_t n)
+{
+    const size_t lane = (size_t)blockIdx.x * kThreads + threadIdx.x;
+    if constexpr (VEC && P2 > 0) {
+        constexpr int V = Pack<T>::N;
+        const size_t i0 = lane * V;
+        if (i0 + V <= n) {
+            u32x4 lv[P2], xv[P2];
+#pragma unroll
+            for (int y = 0; y < P2; ++y) {
+                lv[y] = reinterpret_cast<const u32x4 *>(a.leaf[y])[lane];
+                if (a.extra[y]) xv[y] = reinterpret_cast<const u32x4 *>(a.extra[y])[lane];
+            }
+            Pack<T> r;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                T v[P2];
+#pragma unroll
+                for (int y = 0; y < P2; ++y) {
+                    v[y] = __builtin_bit_cast(Pack<T>, lv[y]).e[j];
+                    if (a.extra[y]) v[y] = OP::f(v[y], __builtin_bit_cast(Pack<T>, xv[y]).e[j]);
+                }
+                r.e[j] = fold_elem<T, OP, P2, SOSX_ORDER_TREE>(v);
+            }
+            store_pack<T>(out, i0, r, a.vec_out != 0);
+        } else {
+            for (size_t i = i0; i < n; ++i) out[i] = small_tree_elem<T, OP, P2>(a, i);
+        }
+    } else {
+        if (lane < n) out[lane] = small_tree_elem<T, OP, P2>(a, lane);
+    }
+    signal_done(a.flags, a.seq);
+}
+
+// The ring's value of every element: element i of ring chunk c is the LINEAR fold
+// ((in[c] OP in[c+1]) OP ...) OP in[c-1] (the reduce-scatter's order, src/collectives.c:
+// 693-727; chunk math :697-709), and every PE evaluates every chunk (the allgather's
+// result, :737-756).  Workgroups are dealt per chunk, so the rotation is uniform per
+// workgroup.  In chunk c, the first workgroup also takes the `head` elements before
+// the first 16-B boundary and the elements after the last whole vector.
+struct SmallRingArgs {
+    const void *in[8];    // team order
+    uint64_t first[9];    // chunk c = elements [first[c], first[c + 1])
+    uint64_t head[8];     // elements of chunk c before its first vector
+    uint64_t nvec[8];     // whole vectors of chunk c (VEC) or its elements (not VEC)
+    uint64_t tstart[9];   // chunk c = workgroups [tstart[c], tstart[c + 1])
+    uint32_t *flags;
+    uint32_t seq;
+    int vec_out;
+};
+
+template <class T, class OP, int NP>
+__device__ __forceinline__ T ring_elem(const SmallRingArgs &a, int c, size_t i)
+{
+    T v[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const int pe = c + k < NP ? c + k : c + k - NP;
+        v[k] = ((const T *)a.in[pe])[i];
+    }
+    return fold_elem<T, OP, NP, SOSX_ORDER_LINEAR>(v);
+}
+
+template <class T, class OP, int NP, bool VEC>
+__global__ __launch_bounds__(kThreads) void k_small_ring(T *out, SmallRingArgs a)
+{
+    const uint64_t b = blockIdx.x;
+    int c = 0;
+    while (b >= a.tstart[c + 1]) ++c;
+    const uint64_t local = b - a.tstart[c];
+    const uint64_t j = local * kThreads + threadIdx.x;
+    if constexpr (VEC) {
+        constexpr int V = Pack<T>::N;
+        const uint64_t body = a.first[c] + a.head[c];
+        if (j < a.nvec[c]) {
+            const size_t i0 = body + j * V;
+            u32x4 x[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const int pe = c + k < NP ? c + k : c + k - NP;
+                x[k] = reinterpret_cast<const u32x4 *>((const T *)a.in[pe] + i0)[0];
+            }
+            Pack<T> r = __builtin_bit_cast(Pack<T>, fold_pack<T, OP, NP, SOSX_ORDER_LINEAR>(x));
+            store_pack<T>(out, i0, r, a.vec_out != 0);
+        }
+        if (local == 0) {
+            for (uint64_t i = a.first[c] + threadIdx.x; i < body; i += kThreads)
+                out[i] = ring_elem<T, OP, NP>(a, c, i);
+            for (uint64_t i = body + a.nvec[c] * V + threadIdx.x; i < a.first[c + 1]; i += kThreads)
+                out[i] = ring_elem<T, OP, NP>(a, c, i);
+        }
+    } else {
+        if (j < a.nvec[c]) out[a.first[c] + j] = ring_elem<T, OP, NP>(a, c, a.first[c] + j);
+    }
+    signal_done(a.flags, a.seq);
+}
+
+}  // namespace sos
+
+using namespace sos;
+
+namespace {
+
+struct SmallFoldFn {
+    template <class T, class OP>
+    static int run(void *out, const SmallFoldArgs *a, size_t n, bool vec, unsigned blocks, hipStream_t st)
+    {
+        switch (a->p2) {
+#define SOS_SMALL(P2)                                                                              \
+    case P2:                                                                                       \
+        if (vec)                                                                                   \
+            hipLaunchKernelGGL((k_small_fold<T, OP, P2, true>), dim3(blocks), dim3(kThreads), 0, st, \
+                               (T *)out, *a, n);                                                   \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_small_fold<T, OP, P2, false>), dim3(blocks), dim3(kThreads), 0, st, \
+                               (T *)out, *a, n);                                                   \
+        break;
+            SOS_SMALL(1)
+            SOS_SMALL(2)
+            SOS_SMALL(4)
+            SOS_SMALL(8)
+#undef SOS_SMALL
+            default:
+                hipLaunchKernelGGL((k_small_fold<T, OP, 0, false>), dim3(blocks), dim3(kThreads), 0, st,
+                                   (T *)out, *a, n);
+        }
+        return hip_ok(hipGetLastError());
+    }
+};
+
+struct SmallRingFn {
+    template <class T, class OP>
+    static int run(void *out, const SmallRingArgs *a, int np, bool vec, unsigned blocks, hipStream_t st)
+    {
+        switch (np) {
+#define SOS_RING(NP)                                                                               \
+    case NP:                                                                                       \
+        if (vec)                                                                                   \
+            hipLaunchKernelGGL((k_small_ring<T, OP, NP, true>), dim3(blocks), dim3(kThreads), 0, st, \
+                               (T *)out, *a);                                                      \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_small_ring<T, OP, NP, false>), dim3(blocks), dim3(kThreads), 0, st, \
+                               (T *)out, *a);                                                      \
+        break;
+            SOS_RING(2)
+            SOS_RING(3)
+            SOS_RING(4)
+            SOS_RING(5)
+            SOS_RING(6)
+            SOS_RING(7)
+            SOS_RING(8)
+#undef SOS_RING
+            default:
+                return SOSX_ERR_ARG;
+        }
+        return hip_ok(hipGetLastError());
+    }
+};
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+// One PE's recdbl_sw value over p2 leaves (leaves[y], each folded first with extras[y]
+// when that is not null), written to `out`; workgroup b then stores `seq` into flags[b]
+// (pinned host memory), b < *nblocks.  count <= SOSX_SMALL_FOLD_MAX.
+int sosx_small_fold(int op, int dtype, void *out, const void *const *leaves,
+                    const void *const *extras, int p2, size_t count, uint32_t *flags, uint32_t seq,
+                    int *nblocks, void *stream)
+{
+    if (p2 < 1 || p2 > SOSX_MAX_FOLD || (p2 & (p2 - 1)) || count > SOSX_SMALL_FOLD_MAX || !flags ||
+        !nblocks)
+        return SOSX_ERR_ARG;
+    int rc = sos_check_op(op, dtype);
+    if (rc) return rc;
+    *nblocks = 0;
+    if (count == 0) return SOSX_OK;
+    if (!out || !leaves) return SOSX_ERR_ARG;
+    SmallFoldArgs a;
+    memset(&a, 0, sizeof(a));
+    bool vec = p2 <= 8;
+    for (int y = 0; y < p2; ++y) {
+        if (!leaves[y]) return SOSX_ERR_ARG;
+        a.leaf[y] = leaves[y];
+        a.extra[y] = extras ? extras[y] : nullptr;
+        vec &= aligned16(a.leaf[y]) && (!a.extra[y] || aligned16(a.extra[y]));
+    }
+    a.flags = flags;
+    a.seq = seq;
+    a.p2 = p2;
+    a.vec_out = aligned16(out);
+    const size_t V = vec ? 16 / sos_dtype_info(dtype).size : 1;
+    const size_t lanes = (count + V - 1) / V;
+    const unsigned blocks = (unsigned)((lanes + kThreads - 1) / kThreads);
+    *nblocks = (int)blocks;
+    return dispatch<SmallFoldFn>(op, dtype, out, (const SmallFoldArgs *)&a, count, vec, blocks,
+                                 as_stream(stream));
+}
+
+// Every element's SOS ring value for one PE (np = 2..8 team operands in team order),
+// written to `out` (count elements); workgroup b then stores `seq` into flags[b],
+// b < *nblocks.
+int sosx_small_ring(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
+                    uint32_t *flags, uint32_t seq, int *nblocks, void *stream)
+{
+    if (np < 2 || np > 8 || count > SOSX_SMALL_FOLD_MAX || !flags || !nblocks) return SOSX_ERR_ARG;
+    int rc = sos_check_op(op, dtype);
+    if (rc) return rc;
+    *nblocks = 0;
+    if (count == 0) return SOSX_OK;
+    if (!out || !ins) return SOSX_ERR_ARG;
+    SmallRingArgs a;
+    memset(&a, 0, sizeof(a));
+    bool vec = true;
+    for (int c = 0; c < np; ++c) {
+        if (!ins[c]) return SOSX_ERR_ARG;
+        a.in[c] = ins[c];
+        vec &= aligned16(ins[c]);
+    }
+    const uint64_t V = vec ? 16 / sos_dtype_info(dtype).size : 1;
+    const uint64_t q = count / (uint64_t)np, r = count % (uint64_t)np;
+    uint64_t first = 0, tiles = 0;
+    for (int c = 0; c < np; ++c) {
+        const uint64_t len = q + ((uint64_t)c < r ? 1 : 0);  // src/collectives.c:697-709
+        a.first[c] = first;
+        a.tstart[c] = tiles;
+        uint64_t head = vec ? (V - first % V) % V : 0;
+        if (head > len) head = len;
+        a.head[c] = head;
+        a.nvec[c] = (len - head) / V;
+        if (len) tiles += a.nvec[c] ? (a.nvec[c] + kThreads - 1) / kThreads : 1;
+        first += len;
+    }
+    a.first[np] = first;
+    a.tstart[np] = tiles;
+    for (int c = np + 1; c <= 8; ++c) {  // sentinels: the chunk search never passes np
+        a.first[c] = first;
+        a.tstart[c] = ~(uint64_t)0;
+    }
+    a.flags = flags;
+    a.seq = seq;
+    a.vec_out = aligned16(out);
+    *nblocks = (int)tiles;
+    return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles,
+                                 as_stream(stream));
+}
+
+}  // extern "C"

@@ -44,8 +44,27 @@ namespace sosrt {
 namespace {
 
 constexpr int kMaxPE = 64;
-constexpr size_t kSlotBytes = 64 * 1024;  // the largest operand this path takes
-constexpr size_t kFlagWords = kSlotBytes / 256;  // one per workgroup of a 1-byte-type fold
+constexpr size_t kSlotsCap = (size_t)32 << 20;  // all PEs' two slots together
+constexpr size_t kRingMaxPE = 8;                // sosx_small_ring's team sizes
+// A call reads P operands over the host link (staging moves 2 per PE) after a host
+// memcpy of its own, so above about a MiB per PE staging + the exchange wins: measured
+// with P PEs on one GPU (profiles/r3_small_latency.txt, crossover runs), P = 2 at 256 KiB
+// operands 50 us here vs 98 staged, at 1 MiB 231 vs 157; P = 4 at 256 KiB 141 vs 186.
+// The path takes P * bytes <= this.
+constexpr size_t kTeamBytes = (size_t)1 << 20;
+constexpr size_t kLatencyBytes = 16 * 1024;     // always taken when it fits a slot
+
+// Slot bytes (the largest operand the path takes): SHMEMX_SMALL_HOST_BYTES (default
+// 1 MiB), capped so that 2 slots per PE stay within kSlotsCap, in 4 KiB units, at
+// most SOSX_SMALL_FOLD_MAX 1-byte elements.  The same on every PE (job environment).
+size_t slot_bytes_for(int npes)
+{
+    size_t b = env_size("SHMEMX_SMALL_HOST_BYTES", (size_t)1 << 20);
+    const size_t cap = kSlotsCap / (2 * (size_t)(npes > 0 ? npes : 1));
+    if (b > cap) b = cap;
+    if (b > (size_t)SOSX_SMALL_FOLD_MAX) b = SOSX_SMALL_FOLD_MAX;
+    return (b + 4095) & ~(size_t)4095;
+}
 
 struct alignas(64) PairWord {
     std::atomic<uint64_t> v;
@@ -66,6 +85,7 @@ struct Small {
     char *host = nullptr;        // region base (host view)
     char *dev = nullptr;         // the same bytes, device view
     size_t bytes = 0;
+    size_t slot = 0;             // bytes per data slot
     int npes = 0;
     uint64_t seq = 0;            // my posts (slot = seq % 2)
     uint64_t posted_to[kMaxPE] = {0};
@@ -82,7 +102,7 @@ size_t ctl_bytes(int npes) { return ((size_t)npes * sizeof(SmallCtl) + 4095) & ~
 
 SmallCtl *ctl(int pe) { return (SmallCtl *)(g.host + (size_t)pe * sizeof(SmallCtl)); }
 
-size_t slot_off(int pe, int sl) { return ctl_bytes(g.npes) + ((size_t)pe * 2 + (size_t)sl) * kSlotBytes; }
+size_t slot_off(int pe, int sl) { return ctl_bytes(g.npes) + ((size_t)pe * 2 + (size_t)sl) * g.slot; }
 
 double limit_s()
 {
@@ -146,7 +166,7 @@ void wait_flags(int nb, uint32_t seq, const char *fn)
 size_t small_shared_bytes(int npes)
 {
     if (npes < 2 || npes > kMaxPE) return 0;
-    return ctl_bytes(npes) + (size_t)npes * 2 * kSlotBytes;
+    return ctl_bytes(npes) + (size_t)npes * 2 * slot_bytes_for(npes);
 }
 
 // Collective (init_common, every PE): register this PE's view of the region with HIP
@@ -159,6 +179,8 @@ void small_path_setup(void *region, size_t bytes)
     const bool want = !(e && !strcmp(e, "0"));
     if (!s.hub.up || s.n_pes < 2 || s.n_pes > kMaxPE) return;
     int ok = region != nullptr && bytes >= small_shared_bytes(s.n_pes) && want;
+    const size_t slot = slot_bytes_for(s.n_pes);
+    const size_t flag_words = slot / 256 + kRingMaxPE;  // a 1-byte fold's workgroups
     void *dptr = nullptr;
     if (ok) {
         if (hipHostRegister(region, bytes, kP2PHostRegisterFlags) == hipSuccess) {
@@ -169,17 +191,17 @@ void small_path_setup(void *region, size_t bytes)
         }
         if (!ok) (void)hipGetLastError();
     }
-    if (ok && hipHostMalloc(&g.out, kSlotBytes, hipHostMallocDefault) != hipSuccess) {
+    if (ok && hipHostMalloc(&g.out, slot, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         g.out = nullptr;
         ok = 0;
     }
-    if (ok && hipHostMalloc((void **)&g.flags, kFlagWords * sizeof(uint32_t), hipHostMallocCoherent) != hipSuccess) {
+    if (ok && hipHostMalloc((void **)&g.flags, flag_words * sizeof(uint32_t), hipHostMallocCoherent) != hipSuccess) {
         (void)hipGetLastError();
         g.flags = nullptr;
         ok = 0;
     }
-    if (g.flags) memset(g.flags, 0, kFlagWords * sizeof(uint32_t));
+    if (g.flags) memset(g.flags, 0, flag_words * sizeof(uint32_t));
     std::vector<int> oks((size_t)s.n_pes);
     if (sosboot::hub_allgather(&s.hub, &ok, sizeof(ok), oks.data()) != 0)
         raise_error("shmem_init: small-path agreement failed");
@@ -187,6 +209,7 @@ void small_path_setup(void *region, size_t bytes)
     g.host = (char *)region;
     g.dev = (char *)dptr;
     g.bytes = bytes;
+    g.slot = slot;
     g.npes = s.n_pes;
     g.ready = ok != 0;
     if (!g.ready) small_path_teardown();
@@ -206,15 +229,21 @@ long small_path_calls() { return g.calls; }
 // Does a reduction of `bytes` with these operands over team t take the small path?
 bool small_path_takes(int alg, const void *target, const void *source, size_t bytes, const Team &t)
 {
-    if (!g.ready || bytes == 0 || bytes > kSlotBytes || t.size < 2 || t.size > kMaxPE) return false;
-    if (alg != SOSX_ALG_RECDBL && alg != SOSX_ALG_RECDBL_GATHER) return false;
+    if (!g.ready || bytes == 0 || bytes > g.slot || t.size < 2 || t.size > kMaxPE) return false;
+    if (bytes > kLatencyBytes && (size_t)t.size * bytes > kTeamBytes) return false;
+    if (alg == SOSX_ALG_RING) {
+        if ((size_t)t.size > kRingMaxPE) return false;
+    } else if (alg != SOSX_ALG_RECDBL && alg != SOSX_ALG_RECDBL_GATHER) {
+        return false;
+    }
     if (sosplan::pow2_floor(t.size) > SOSX_MAX_FOLD) return false;
     return !is_device_ptr(source) && !is_device_ptr(target);
 }
 
-// recdbl_sw's value for this PE over team t (see the file comment); returns when done.
-void small_path_reduce(void *target, const void *source, size_t count, size_t ts, const Team &t,
-                       int op, int dt, const char *fn)
+// recdbl_sw's (or, for alg RING, the ring's) value for this PE over team t (see the
+// file comment); returns when done.
+void small_path_reduce(int alg, void *target, const void *source, size_t count, size_t ts,
+                       const Team &t, int op, int dt, const char *fn)
 {
     State &s = st();
     const size_t bytes = count * ts;
@@ -235,44 +264,50 @@ void small_path_reduce(void *target, const void *source, size_t count, size_t ts
         mine->posted[r].v.store(k, std::memory_order_release);
         g.slot_users[sl].push_back({r, k});
     }
-    std::vector<const void *> in((size_t)P);
-    std::vector<int> from((size_t)P, -1);
+    const void *in[kMaxPE];
+    int from[kMaxPE];
     for (int i = 0; i < P; ++i) {
+        from[i] = -1;
         const int q = t.world_rank(i);
         if (i == me) {
-            in[(size_t)i] = g.dev + slot_off(mw, sl);
+            in[i] = g.dev + slot_off(mw, sl);
             continue;
         }
         const uint64_t k = ++g.seen_from[q];
         wait_ge(ctl(q)->posted[mw].v, k, "a peer's operand");
         const int qs = (int)ctl(q)->ring[mw][k % 2];
-        in[(size_t)i] = g.dev + slot_off(q, qs);
-        from[(size_t)i] = q;
-    }
-    // 3. one launch: this PE's recdbl_sw tree over the leaves w[y] = v[y ^ mp], where
-    //    v[x] = in[x] OP in[x + p2] for the extra PEs (x < P - p2), else in[x]
-    const int p2 = sosplan::pow2_floor(P), nx = P - p2;
-    const int mp = me < p2 ? me : me - p2;
-    std::vector<const void *> leaves((size_t)p2), extras((size_t)p2);
-    for (int y = 0; y < p2; ++y) {
-        const int x = y ^ mp;
-        leaves[(size_t)y] = in[(size_t)x];
-        extras[(size_t)y] = x < nx ? in[(size_t)(x + p2)] : nullptr;
+        in[i] = g.dev + slot_off(q, qs);
+        from[i] = q;
     }
     // the result goes straight into the host symmetric heap (device-mapped pinned
     // memory), else into the pinned result slot
     const bool direct = s.host_heap.contains(target, bytes);
     void *out = direct ? target : g.out;
     if (++g.fseq == 0) g.fseq = 1;
-    const int rc = sosx_small_fold(op, dt, out, leaves.data(), extras.data(), p2, count, g.flags, g.fseq,
-                                   s.stream);
+    int rc, nblocks = 0;
+    if (alg == SOSX_ALG_RING) {
+        // 3. one launch: every ring chunk c folded LINEAR from PE c (the reduce-scatter's
+        //    order), all chunks by every PE (the allgather's result)
+        rc = sosx_small_ring(op, dt, out, in, P, count, g.flags, g.fseq, &nblocks, s.stream);
+    } else {
+        // 3. one launch: this PE's recdbl_sw tree over the leaves w[y] = v[y ^ mp], where
+        //    v[x] = in[x] OP in[x + p2] for the extra PEs (x < P - p2), else in[x]
+        const int p2 = sosplan::pow2_floor(P), nx = P - p2;
+        const int mp = me < p2 ? me : me - p2;
+        const void *leaves[kMaxPE], *extras[kMaxPE];
+        for (int y = 0; y < p2; ++y) {
+            const int x = y ^ mp;
+            leaves[y] = in[x];
+            extras[y] = x < nx ? in[x + p2] : nullptr;
+        }
+        rc = sosx_small_fold(op, dt, out, leaves, extras, p2, count, g.flags, g.fseq, &nblocks, s.stream);
+    }
     if (rc) raise_error("%s: small host-resident reduction failed (status %d)", fn, rc);
     // 4. completion from the workgroups' flags (no stream synchronisation); then the
     //    peers' slots are read: acknowledge; my result out
-    wait_flags((int)((count + 255) / 256), g.fseq, fn);
+    wait_flags(nblocks, g.fseq, fn);
     for (int i = 0; i < P; ++i)
-        if (from[(size_t)i] >= 0)
-            mine->consumed[from[(size_t)i]].v.store(g.seen_from[from[(size_t)i]], std::memory_order_release);
+        if (from[i] >= 0) mine->consumed[from[i]].v.store(g.seen_from[from[i]], std::memory_order_release);
     if (!direct) memcpy(target, g.out, bytes);
     g.calls++;
 }

@@ -218,9 +218,26 @@ def test_small_fold_rejects_bad_args():
     L = _lib.lib()
     one = (ctypes.c_void_p * 1)(1)
     flags = 1
-    assert L.sosx_small_fold(5, 23, None, one, None, 3, 1, flags, 1, None) == -3       # p2 not pow2
-    assert L.sosx_small_fold(5, 23, None, one, None, 1, 65537, flags, 1, None) == -3   # too long
-    assert L.sosx_small_fold(5, 23, None, one, None, 1, 1, None, 1, None) == -3        # no flags
-    assert L.sosx_small_fold(0, 23, None, one, None, 1, 1, flags, 1, None) == -2       # and on float
-    assert L.sosx_small_fold(5, 0, None, one, None, 1, 1, flags, 1, None) == -1        # SIGNED_BYTE
-    assert L.sosx_small_fold(5, 23, None, one, None, 1, 0, flags, 1, None) == 0        # count 0
+    nb = ctypes.byref(ctypes.c_int(-1))
+    assert L.sosx_small_fold(5, 23, None, one, None, 3, 1, flags, 1, nb, None) == -3       # p2 not pow2
+    assert L.sosx_small_fold(5, 23, None, one, None, 1, (1 << 20) + 1, flags, 1, nb, None) == -3
+    assert L.sosx_small_fold(5, 23, None, one, None, 1, 1, None, 1, nb, None) == -3        # no flags
+    assert L.sosx_small_fold(5, 23, None, one, None, 1, 1, flags, 1, None, None) == -3     # no nblocks
+    assert L.sosx_small_fold(0, 23, None, one, None, 1, 1, flags, 1, nb, None) == -2       # and on float
+    assert L.sosx_small_fold(5, 0, None, one, None, 1, 1, flags, 1, nb, None) == -1        # SIGNED_BYTE
+    assert L.sosx_small_fold(5, 23, None, one, None, 1, 0, flags, 1, nb, None) == 0        # count 0
+
+
+def test_small_ring_rejects_bad_args():
+    """sosx_small_ring validates before any device work (CPU)."""
+    import ctypes
+    from sos_amd import _lib
+    L = _lib.lib()
+    ins = (ctypes.c_void_p * 9)(*([1] * 9))
+    nb = ctypes.c_int(-1)
+    assert L.sosx_small_ring(5, 23, None, ins, 1, 1, 1, 1, ctypes.byref(nb), None) == -3        # np < 2
+    assert L.sosx_small_ring(5, 23, None, ins, 9, 1, 1, 1, ctypes.byref(nb), None) == -3        # np > 8
+    assert L.sosx_small_ring(5, 23, None, ins, 2, (1 << 20) + 1, 1, 1, ctypes.byref(nb), None) == -3
+    assert L.sosx_small_ring(5, 23, None, ins, 2, 1, None, 1, ctypes.byref(nb), None) == -3      # no flags
+    assert L.sosx_small_ring(0, 24, None, ins, 2, 1, 1, 1, ctypes.byref(nb), None) == -2         # and on double
+    assert L.sosx_small_ring(5, 23, None, ins, 2, 0, 1, 1, ctypes.byref(nb), None) == 0 and nb.value == 0

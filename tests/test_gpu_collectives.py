@@ -233,39 +233,106 @@ def _perspective_inputs(dt, P, n, seed):
     return srcs
 
 
+def _pinned(torch, raw, offset):
+    """A pinned host buffer holding `raw` bytes `offset` bytes past a 16-B boundary."""
+    buf = torch.zeros(raw.size + 64, dtype=torch.uint8, pin_memory=True)
+    base = (-buf.data_ptr()) % 16 + offset
+    buf[base:base + raw.size] = torch.from_numpy(raw.copy())
+    return buf, buf.data_ptr() + base
+
+
+LAYOUTS = ["aligned", "in_misaligned", "out_misaligned"]
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("P", [2, 3, 4, 5, 7, 8, 12, 16])
 @pytest.mark.parametrize("dt,op", [(23, 5), (24, 4), (23, 3), (4, 3), (27, 6), (25, 5), (1, 6)])
-def test_small_fold_kernel(torch_cuda, P, dt, op):
+def test_small_fold_kernel(torch_cuda, P, dt, op, layout):
     """sosx_small_fold (the small host-resident path's one launch): operands, result and
     completion words all in pinned host memory, every PE's own recdbl_sw value (oracle
-    recdbl, per PE: +-0 ties and NaN payloads included), and every workgroup's
-    completion word set to the call's sequence number."""
+    recdbl, per PE: +-0 ties and NaN payloads included).  Aligned operands take the
+    16-B-vector lanes; a misaligned operand the element lanes; a misaligned result vector
+    loads with element stores.  Exactly the first *nblocks completion words carry the
+    call's sequence number."""
     import ctypes
     torch = torch_cuda
     L = _lib.lib()
     p2 = 1 << (P.bit_length() - 1)
     nx = P - p2
-    flags = torch.zeros(256, dtype=torch.int32, pin_memory=True)
+    flags = torch.zeros(4096 + 8, dtype=torch.int32, pin_memory=True)
     seq = 0
-    for n in (1, 255, 257, 4095):
+    for n in (1, 255, 257, 4095, 20001):
         srcs = _perspective_inputs(dt, P, n, seed=n + P)
         ref = O.recdbl(op, dt, srcs)
-        host = [torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory() for a in srcs]
-        out = torch.zeros(srcs[0].nbytes, dtype=torch.uint8, pin_memory=True)
+        es = srcs[0].itemsize
+        keep, ptr = [], []
+        for p, a in enumerate(srcs):
+            b, q = _pinned(torch, np.frombuffer(a.tobytes(), np.uint8),
+                           es if (layout == "in_misaligned" and p == P - 1 and es < 16) else 0)
+            keep.append(b)
+            ptr.append(q)
+        ob, optr = _pinned(torch, np.zeros(srcs[0].nbytes, np.uint8),
+                           es if (layout == "out_misaligned" and es < 16) else 0)
         for me in sorted({0, P // 2, P - 1}):
             mp = me if me < p2 else me - p2
-            leaves = [host[y ^ mp].data_ptr() for y in range(p2)]
-            extras = [host[(y ^ mp) + p2].data_ptr() if (y ^ mp) < nx else None for y in range(p2)]
+            leaves = [ptr[y ^ mp] for y in range(p2)]
+            extras = [ptr[(y ^ mp) + p2] if (y ^ mp) < nx else None for y in range(p2)]
             seq += 1
-            out.fill_(0xA5)
-            rc = L.sosx_small_fold(op, dt, ctypes.c_void_p(out.data_ptr()),
+            ob.fill_(0xA5)
+            nb = ctypes.c_int(-1)
+            rc = L.sosx_small_fold(op, dt, ctypes.c_void_p(optr),
                                    (ctypes.c_void_p * p2)(*leaves), (ctypes.c_void_p * p2)(*extras),
                                    p2, ctypes.c_size_t(n), ctypes.c_void_p(flags.data_ptr()),
-                                   ctypes.c_uint32(seq), None)
+                                   ctypes.c_uint32(seq), ctypes.byref(nb), None)
             assert rc == 0
             torch.cuda.synchronize()
-            nb = (n + 255) // 256
-            assert bool((flags[:nb] == seq).all()), (n, me, flags[:nb].tolist())
-            got = np.frombuffer(out.numpy().tobytes(), srcs[0].dtype)
-            assert np.array_equal(bits(got), bits(ref[me])), (P, dt, op, n, me)
+            assert 1 <= nb.value <= (n + 255) // 256
+            assert bool((flags[:nb.value] == seq).all()) and int(flags[nb.value]) != seq, (n, me)
+            off = optr - ob.data_ptr()
+            got = np.frombuffer(ob[off:off + srcs[0].nbytes].numpy().tobytes(), srcs[0].dtype)
+            assert np.array_equal(bits(got), bits(ref[me])), (P, dt, op, n, me, layout)
 
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("dt,op", [(23, 5), (24, 4), (23, 3), (4, 6), (27, 6), (25, 5), (1, 5)])
+def test_small_ring_kernel(torch_cuda, P, dt, op, layout):
+    """sosx_small_ring (the small host-resident path above the crossover): operands,
+    result and completion words in pinned host memory; every element equals SOS's ring
+    result (oracle ring: chunk c folded from PE c, src/collectives.c:693-727), ragged
+    sizes included (n < P leaves chunks empty, chunk starts off the 16-B grid); aligned,
+    misaligned-operand and misaligned-result layouts; exactly the first *nblocks
+    completion words carry the call's sequence number."""
+    import ctypes
+    torch = torch_cuda
+    L = _lib.lib()
+    flags = torch.zeros(4096 + 8, dtype=torch.int32, pin_memory=True)
+    seq = 0
+    for n in (1, P - 1, 7, 255 * P + 3, 4097, 65536 + 5):
+        if n < 1:
+            continue
+        srcs = _perspective_inputs(dt, P, n, seed=2 * n + P)
+        ref = O.ring(op, dt, srcs)
+        for p in range(1, P):
+            assert np.array_equal(bits(ref[p]), bits(ref[0]))
+        es = srcs[0].itemsize
+        keep, ptr = [], []
+        for p, a in enumerate(srcs):
+            b, q = _pinned(torch, np.frombuffer(a.tobytes(), np.uint8),
+                           es if (layout == "in_misaligned" and p == 0 and es < 16) else 0)
+            keep.append(b)
+            ptr.append(q)
+        ob, optr = _pinned(torch, np.full(srcs[0].nbytes, 0xA5, np.uint8),
+                           es if (layout == "out_misaligned" and es < 16) else 0)
+        seq += 1
+        nb = ctypes.c_int(-1)
+        rc = L.sosx_small_ring(op, dt, ctypes.c_void_p(optr), (ctypes.c_void_p * P)(*ptr), P,
+                               ctypes.c_size_t(n), ctypes.c_void_p(flags.data_ptr()),
+                               ctypes.c_uint32(seq), ctypes.byref(nb), None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert 1 <= nb.value <= (n + 255) // 256 + P
+        assert bool((flags[:nb.value] == seq).all()) and int(flags[nb.value]) != seq, n
+        off = optr - ob.data_ptr()
+        got = np.frombuffer(ob[off:off + srcs[0].nbytes].numpy().tobytes(), srcs[0].dtype)
+        assert np.array_equal(bits(got), bits(ref[0])), (P, dt, op, n, layout)

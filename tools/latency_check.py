@@ -12,6 +12,11 @@ collective).  Legs:
           barrier per call (the team API's pSync reuse rule) -- the reference baseline
 Schedules: recdbl (recdbl_sw butterfly), recdbl_gather (one all-gather round + every
 PE's own tree: AUTO below the crossover), ring (AUTO above it).
+
+--crossover: host-heap operands through the library under AUTO, and SOS's CPU under its
+own AUTO rule (recdbl_sw below SHMEM_COLL_SIZE_CROSSOVER = 16 KiB, ring above,
+src/shmem_collectives.h:180-199), from 16 KiB to 16 MiB: where the GPU path starts to
+win for SOS's own (host-resident) operands.
 """
 import argparse
 import ctypes
@@ -29,6 +34,7 @@ from sos_amd import _lib as L  # noqa: E402
 from sos_amd import shmem as S  # noqa: E402
 
 SMALL = [1, 64, 1024, 4095]      # fp32: up to 16380 B, below the 16 KiB crossover
+CROSS = [4095, 16384, 65536, 262144, 1 << 20, 1 << 22]   # fp32: 16 KiB .. 16 MiB
 
 
 def max_over_pes(v, scratch):
@@ -49,8 +55,10 @@ def time_calls(fn, reps):
     return (time.perf_counter() - t0) / reps
 
 
-def cpu_leg(me, P, reps, scratch):
-    """SOS's recdbl_sw on the CPU, one pinned physical core per PE."""
+def cpu_leg(me, P, reps, scratch, sizes=None):
+    """SOS's recdbl_sw on the CPU, one pinned physical core per PE (with `sizes`: SOS's
+    AUTO choice per size, recdbl_sw below 16 KiB and ring above, `reps` scaled down for
+    large sizes)."""
     from oracle import oracle as O
     allowed = sorted(os.sched_getaffinity(0))
     prim = []
@@ -63,7 +71,9 @@ def cpu_leg(me, P, reps, scratch):
         if first == c or first not in allowed:
             prim.append(c)
     path = f"/dev/shm/sosx_lat_{os.getppid()}_{P}"
-    nmax = max(SMALL)
+    auto = sizes is not None
+    sizes = sizes or SMALL
+    nmax = max(sizes)
     if me == 0:
         if os.path.exists(path):
             os.unlink(path)
@@ -78,10 +88,13 @@ def cpu_leg(me, P, reps, scratch):
     out = {}
     os.sched_setaffinity(0, {prim[me % len(prim)]})
     try:
-        for n in SMALL:
+        for n in sizes:
             ring.count = n
-            ring.time(5, src, 100)                 # warm-up
-            t = ring.time(5, src, reps) / reps
+            if auto:
+                ring.alg = PeAlg.RECDBL if n * 4 < 16384 else PeAlg.RING
+            r = max(10, min(reps, int(reps * 4096 / max(n, 4096))))
+            ring.time(5, src, max(5, r // 10))     # warm-up
+            t = ring.time(5, src, r) / r
             out[n] = t
     finally:
         os.sched_setaffinity(0, set(allowed))
@@ -90,11 +103,17 @@ def cpu_leg(me, P, reps, scratch):
     return {n: max_over_pes(t, scratch) for n, t in out.items()}, prim[0]
 
 
+class PeAlg:
+    RING, RECDBL = 0, 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--legs", default="dev,host,cpu")
     ap.add_argument("--reps", type=int, default=int(os.environ.get("LAT_REPS", "200")))
     ap.add_argument("--ring", action="store_true", help="also the ring above the crossover (dev)")
+    ap.add_argument("--crossover", action="store_true",
+                    help="host-heap AUTO vs SOS CPU AUTO from 16 KiB to 16 MiB (replaces the legs)")
     a = ap.parse_args()
     S.shmem_init()
     me, P = S.shmem_my_pe(), S.shmem_n_pes()
@@ -104,6 +123,22 @@ def main():
     nmax = max(ring_sizes)
     scratch = S.lib().shmem_malloc(64)
     rows = []
+    if a.crossover:
+        legs = []
+        nmx = max(CROSS)
+        hs = S.lib().shmem_malloc(nmx * 4)
+        hd = S.lib().shmem_malloc(nmx * 4)
+        np.ctypeslib.as_array((ctypes.c_float * nmx).from_address(hs))[:] = 0.5 + me
+        S.shmemx_set_reduce_algorithm(L.ALGS["auto"])
+        for n in CROSS:
+            r = max(10, min(a.reps, int(a.reps * 4096 / max(n, 4096))))
+            t = time_calls(lambda: S.shmem_float_sum_reduce(team, hd, hs, n), r)
+            rows.append(("host", "auto", n, max_over_pes(t, scratch)))
+        S.lib().shmem_free(hd)
+        S.lib().shmem_free(hs)
+        cpu, core0 = cpu_leg(me, P, max(a.reps * 10, 2000), scratch, sizes=CROSS)
+        for n, t in cpu.items():
+            rows.append(("cpu", "auto(sos)", n, t))
     if "dev" in legs:
         src = S.shmemx_malloc_device(nmax * 4)
         dst = S.shmemx_malloc_device(nmax * 4)
@@ -135,6 +170,10 @@ def main():
     if me == 0:
         for leg, alg, n, t in rows:
             print(f"P={P} {leg:4s} {alg:14s} n={n:7d}: {t * 1e6:8.2f} us/call", flush=True)
+        if a.crossover:
+            print(f"# cpu: SOS AUTO on the CPU (oracle_pe_recdbl below 16 KiB, oracle_pe_ring above), "
+                  f"{P} processes pinned to consecutive physical cores from {core0}, barrier per call",
+                  flush=True)
         if "cpu" in legs:
             print(f"# cpu: oracle_pe_recdbl, {P} processes pinned to consecutive physical cores "
                   f"from {core0}, barrier per call included", flush=True)

@@ -60,8 +60,8 @@ def main():
     maxn = max(SIZES)
     hsrc = S.shmemx_malloc_device(maxn * 16)
     hdst = S.shmemx_malloc_device(maxn * 16)
-    hh_in = S.lib().shmem_malloc(5003 * 16)       # host symmetric heap (pinned)
-    hh_out = S.lib().shmem_malloc(5003 * 16)
+    hh_in = S.lib().shmem_malloc(65536 * 16)      # host symmetric heap (pinned)
+    hh_out = S.lib().shmem_malloc(65536 * 16)
     # an even-PE team (split_strided), when there are at least 3 PEs
     even = ctypes.c_void_p(0)
     if P >= 3:
@@ -83,7 +83,7 @@ def main():
                 seed = zlib.crc32(f"{alg}/{tname}/{oname}/{n}".encode())
                 resolved = S.lib().sosx_resolve_alg(L.ALGS[alg], n * es, 16384)
                 for mode in ("heap", "heap_inplace", "device", "host", "hostheap"):
-                    if mode in ("host", "hostheap") and n > 5003:
+                    if mode in ("host", "hostheap") and n > 65536:
                         continue
                     L.fill(dt, dist, seed, me, hsrc, n)
                     torch.cuda.synchronize()
@@ -132,6 +132,17 @@ def main():
                     checks += 1
                     if mm:
                         bad.append((alg, tname, oname, n, "even_team", mm))
+                    # the same team on the host symmetric heap (small host-resident path)
+                    h_in = _download(hsrc, n * es)
+                    ctypes.memmove(hh_in, h_in.ctypes.data, n * es)
+                    fn(even.value, hh_out, hh_in, n)
+                    h_out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * es)).from_address(hh_out))
+                    tmp = torch.from_numpy(h_out.copy()).cuda()
+                    torch.cuda.synchronize()
+                    mm = L.count_mismatch(exp.data_ptr(), tmp.data_ptr(), n, es)
+                    checks += 1
+                    if mm:
+                        bad.append((alg, tname, oname, n, "even_team_hostheap", mm))
     S.shmem_barrier_all()
     S.shmemx_free_device(hdst)
     S.shmemx_free_device(hsrc)

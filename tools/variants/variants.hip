@@ -543,3 +543,77 @@ extern "C" double sosxv_service_probe(int n, int iters, void *stream)
     (void)hipHostFree(words);
     return ok ? sum / iters : -2.0;
 }
+
+// ---------------------------------------------------------------------------------
+// Kernel reads of host memory by allocation kind (bench only): what the small
+// host-resident path's slots should be.  mode 0: hipHostMalloc coherent; 1: hipHostMalloc
+// non-coherent; 2: mmap + hipHostRegister (fine grained, the small path today);
+// 3: mmap + hipHostRegister(hipExtHostRegisterCoarseGrained).  Every iteration the host
+// writes a new pattern, then ONE kernel reads the whole buffer (16 B per lane) and counts
+// words that do not carry the pattern (stale data after a host write); returns GB/s of
+// the kernel reads (host events around the launch + synchronisation, pattern write not
+// timed) and the stale-word count.
+// ---------------------------------------------------------------------------------
+#include <sys/mman.h>
+
+__global__ __launch_bounds__(256) void k_host_read(const u32x4 *p, size_t nvec, unsigned pat,
+                                                  unsigned long long *bad)
+{
+    unsigned long long b = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (size_t)gridDim.x * 256) {
+        const u32x4 v = p[i];
+        b += (v[0] != pat) + (v[1] != pat) + (v[2] != pat) + (v[3] != pat);
+    }
+    if (b) atomicAdd(bad, b);
+}
+
+extern "C" int sosxv_host_read_probe(int mode, size_t bytes, int iters, double *gbps,
+                                     unsigned long long *stale, void *stream)
+{
+    hipStream_t st = as_stream(stream);
+    void *buf = nullptr;
+    bool mapped = false;
+    if (mode == 0 || mode == 1) {
+        if (hipHostMalloc(&buf, bytes, mode == 0 ? hipHostMallocCoherent : hipHostMallocNonCoherent) != hipSuccess)
+            return -1;
+    } else {
+        buf = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+        if (buf == MAP_FAILED) return -1;
+        mapped = true;
+        const unsigned fl = hipHostRegisterMapped | (mode == 3 ? hipExtHostRegisterCoarseGrained : 0);
+        if (hipHostRegister(buf, bytes, fl) != hipSuccess) {
+            munmap(buf, bytes);
+            return -2;
+        }
+    }
+    void *dptr = buf;
+    if (mapped && hipHostGetDevicePointer(&dptr, buf, 0) != hipSuccess) return -3;
+    unsigned long long *bad = nullptr;
+    if (hipMalloc((void **)&bad, 8) != hipSuccess) return -4;
+    (void)hipMemsetAsync(bad, 0, 8, st);
+    const size_t nvec = bytes / 16;
+    unsigned blocks = (unsigned)((nvec + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    double total = 0;
+    for (int it = -2; it < iters; ++it) {
+        const unsigned pat = 0x1000u + (unsigned)(it + 2);
+        unsigned *w = (unsigned *)buf;
+        for (size_t i = 0; i < bytes / 4; ++i) w[i] = pat;
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        const auto t0 = std::chrono::steady_clock::now();
+        hipLaunchKernelGGL(k_host_read, dim3(blocks), dim3(256), 0, st, (const u32x4 *)dptr, nvec, pat, bad);
+        (void)hipStreamSynchronize(st);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (it >= 0) total += std::chrono::duration<double>(t1 - t0).count();
+    }
+    (void)hipMemcpy(stale, bad, 8, hipMemcpyDeviceToHost);
+    *gbps = (double)bytes * iters / total / 1e9;
+    (void)hipFree(bad);
+    if (mapped) {
+        (void)hipHostUnregister(buf);
+        munmap(buf, bytes);
+    } else {
+        (void)hipHostFree(buf);
+    }
+    return 0;
+}
