@@ -163,6 +163,13 @@ int sosx_small_fold(int op, int dtype, void *out, const void *const *leaves,
 int sosx_small_ring(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
                     uint32_t *flags, uint32_t seq, int *nblocks, void *stream);
 
+/* The LINEAR fold ((ins[0] OP ins[1]) OP ...) OP ins[np-1] of np = 1..8 operands in one
+ * launch: one PE's team scan value (inscan: the team's sources 0..me, exscan 0..me-1,
+ * src/collectives.c:1111-1209) on the small host-resident path.  Completion words as
+ * sosx_small_fold. */
+int sosx_small_linear(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
+                      uint32_t *flags, uint32_t seq, int *nblocks, void *stream);
+
 /* Fill `count` elements of device buffer dst with the synthetic input of PE `pe`,
  * element indices [index0, index0 + count).  Bit-identical to the CPU generator
  * (tests/ and bench.py use oracle/sos_oracle.c's oracle_fill). */

@@ -76,6 +76,9 @@ _SIGS = {
     "sosx_small_ring": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _c.POINTER(_c.c_void_p), _c.c_int,
                                    _c.c_size_t, _c.c_void_p, _c.c_uint32, _c.POINTER(_c.c_int),
                                    _c.c_void_p]),
+    "sosx_small_linear": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _c.POINTER(_c.c_void_p), _c.c_int,
+                                     _c.c_size_t, _c.c_void_p, _c.c_uint32, _c.POINTER(_c.c_int),
+                                     _c.c_void_p]),
     "sosx_fill": (_c.c_int, [_c.c_int, _c.c_int, _c.c_uint64, _c.c_int, _c.c_void_p,
                              _c.c_size_t, _c.c_size_t, _c.c_void_p]),
     "sosx_count_mismatch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_size_t,

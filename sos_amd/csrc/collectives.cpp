@@ -771,8 +771,13 @@ int sos_api_scan(shmem_team_t team, void *dest, const void *source, size_t nelem
     if (rc) raise_error("%s: %s (datatype %d, op %d)", fn, status_text(rc), datatype, op);
     if (t->size > sosplan::PLAN_MAX_PE)
         raise_error("%s: teams of more than %d PEs are not supported", fn, sosplan::PLAN_MAX_PE);
-    execute(exclusive ? sosplan::PLAN_EXSCAN : sosplan::PLAN_INSCAN, dest, source, nelems,
-            type_size, *t, op, datatype, fn);
+    const int plan = exclusive ? sosplan::PLAN_EXSCAN : sosplan::PLAN_INSCAN;
+    if (t->size > 1 && small_path_takes(plan, dest, source, bytes, *t)) {
+        // small host-resident operands: one kernel per PE over node shared memory
+        small_path_reduce(plan, dest, source, nelems, type_size, *t, op, datatype, fn);
+        return 0;
+    }
+    execute(plan, dest, source, nelems, type_size, *t, op, datatype, fn);
     return 0;
 }
 

@@ -231,6 +231,7 @@ struct SmallRingFn {
             hipLaunchKernelGGL((k_small_ring<T, OP, NP, false>), dim3(blocks), dim3(kThreads), 0, st, \
                                (T *)out, *a);                                                      \
         break;
+            SOS_RING(1)
             SOS_RING(2)
             SOS_RING(3)
             SOS_RING(4)
@@ -327,6 +328,45 @@ int sosx_small_ring(int op, int dtype, void *out, const void *const *ins, int np
     for (int c = np + 1; c <= 8; ++c) {  // sentinels: the chunk search never passes np
         a.first[c] = first;
         a.tstart[c] = ~(uint64_t)0;
+    }
+    a.flags = flags;
+    a.seq = seq;
+    a.vec_out = aligned16(out);
+    *nblocks = (int)tiles;
+    return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles,
+                                 as_stream(stream));
+}
+
+// The LINEAR fold ((ins[0] OP ins[1]) OP ...) OP ins[np-1] of every element (np = 1..8:
+// the team scans' value at one PE, src/collectives.c:1111-1209 -- inscan folds the team's
+// sources 0..me, exscan 0..me-1), written to `out`; completion words as above.  This is
+// the ring kernel with a single chunk: every workgroup folds from ins[0].
+int sosx_small_linear(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
+                      uint32_t *flags, uint32_t seq, int *nblocks, void *stream)
+{
+    if (np < 1 || np > 8 || count > SOSX_SMALL_FOLD_MAX || !flags || !nblocks) return SOSX_ERR_ARG;
+    int rc = sos_check_op(op, dtype);
+    if (rc) return rc;
+    *nblocks = 0;
+    if (count == 0) return SOSX_OK;
+    if (!out || !ins) return SOSX_ERR_ARG;
+    SmallRingArgs a;
+    memset(&a, 0, sizeof(a));
+    bool vec = true;
+    for (int k = 0; k < np; ++k) {
+        if (!ins[k]) return SOSX_ERR_ARG;
+        a.in[k] = ins[k];
+        vec &= aligned16(ins[k]);
+    }
+    const uint64_t V = vec ? 16 / sos_dtype_info(dtype).size : 1;
+    a.first[0] = 0;
+    a.head[0] = 0;
+    a.nvec[0] = count / V;
+    const uint64_t tiles = a.nvec[0] ? (a.nvec[0] + kThreads - 1) / kThreads : 1;
+    a.tstart[0] = 0;
+    for (int c = 1; c <= 8; ++c) {  // chunk 0 holds everything; the others are empty
+        a.first[c] = count;
+        a.tstart[c] = c <= np ? tiles : ~(uint64_t)0;
     }
     a.flags = flags;
     a.seq = seq;

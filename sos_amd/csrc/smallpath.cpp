@@ -231,7 +231,7 @@ bool small_path_takes(int alg, const void *target, const void *source, size_t by
 {
     if (!g.ready || bytes == 0 || bytes > g.slot || t.size < 2 || t.size > kMaxPE) return false;
     if (bytes > kLatencyBytes && (size_t)t.size * bytes > kTeamBytes) return false;
-    if (alg == SOSX_ALG_RING) {
+    if (alg == SOSX_ALG_RING || sosplan::is_scan(alg)) {
         if ((size_t)t.size > kRingMaxPE) return false;
     } else if (alg != SOSX_ALG_RECDBL && alg != SOSX_ALG_RECDBL_GATHER) {
         return false;
@@ -240,8 +240,8 @@ bool small_path_takes(int alg, const void *target, const void *source, size_t by
     return !is_device_ptr(source) && !is_device_ptr(target);
 }
 
-// recdbl_sw's (or, for alg RING, the ring's) value for this PE over team t (see the
-// file comment); returns when done.
+// recdbl_sw's (or, for alg RING, the ring's; for the scan plans, the scan's) value for
+// this PE over team t (see the file comment); returns when done.
 void small_path_reduce(int alg, void *target, const void *source, size_t count, size_t ts,
                        const Team &t, int op, int dt, const char *fn)
 {
@@ -284,8 +284,15 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     const bool direct = s.host_heap.contains(target, bytes);
     void *out = direct ? target : g.out;
     if (++g.fseq == 0) g.fseq = 1;
-    int rc, nblocks = 0;
-    if (alg == SOSX_ALG_RING) {
+    int rc = SOSX_OK, nblocks = 0;
+    if (sosplan::is_scan(alg)) {
+        // 3. one launch: the in-order prefix of the team's sources 0..me (inscan) or
+        //    0..me-1 (exscan), the running value the left operand; exscan's PE 0 gets
+        //    zeros, as SOS's memset (src/collectives.c:1111-1209)
+        const int np = alg == sosplan::PLAN_INSCAN ? me + 1 : me;
+        if (np == 0) memset(out, 0, bytes);
+        else rc = sosx_small_linear(op, dt, out, in, np, count, g.flags, g.fseq, &nblocks, s.stream);
+    } else if (alg == SOSX_ALG_RING) {
         // 3. one launch: every ring chunk c folded LINEAR from PE c (the reduce-scatter's
         //    order), all chunks by every PE (the allgather's result)
         rc = sosx_small_ring(op, dt, out, in, P, count, g.flags, g.fseq, &nblocks, s.stream);

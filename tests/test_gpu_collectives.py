@@ -336,3 +336,41 @@ def test_small_ring_kernel(torch_cuda, P, dt, op, layout):
         off = optr - ob.data_ptr()
         got = np.frombuffer(ob[off:off + srcs[0].nbytes].numpy().tobytes(), srcs[0].dtype)
         assert np.array_equal(bits(got), bits(ref[0])), (P, dt, op, n, layout)
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("np_", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("dt,op", [(23, 5), (24, 5), (4, 5), (27, 5), (25, 5), (1, 5), (24, 4)])
+def test_small_linear_kernel(torch_cuda, np_, dt, op, layout):
+    """sosx_small_linear (one PE's team scan on the small host-resident path): the
+    in-order LINEAR fold of np operands in pinned host memory equals the oracle's
+    reduce_local prefix (SOS scan_ring order, running value the left operand)."""
+    import ctypes
+    torch = torch_cuda
+    L = _lib.lib()
+    flags = torch.zeros(4096 + 8, dtype=torch.int32, pin_memory=True)
+    seq = 0
+    for n in (1, 7, 4097, 65536 + 5):
+        srcs = _perspective_inputs(dt, np_, n, seed=3 * n + np_)
+        ref = cpu_prefix(op, dt, srcs)[-1]
+        es = srcs[0].itemsize
+        keep, ptr = [], []
+        for p, a in enumerate(srcs):
+            b, q = _pinned(torch, np.frombuffer(a.tobytes(), np.uint8),
+                           es if (layout == "in_misaligned" and p == 0 and es < 16) else 0)
+            keep.append(b)
+            ptr.append(q)
+        ob, optr = _pinned(torch, np.full(srcs[0].nbytes, 0xA5, np.uint8),
+                           es if (layout == "out_misaligned" and es < 16) else 0)
+        seq += 1
+        nb = ctypes.c_int(-1)
+        rc = L.sosx_small_linear(op, dt, ctypes.c_void_p(optr), (ctypes.c_void_p * np_)(*ptr), np_,
+                                 ctypes.c_size_t(n), ctypes.c_void_p(flags.data_ptr()),
+                                 ctypes.c_uint32(seq), ctypes.byref(nb), None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert 1 <= nb.value <= (n + 255) // 256
+        assert bool((flags[:nb.value] == seq).all()) and int(flags[nb.value]) != seq, n
+        off = optr - ob.data_ptr()
+        got = np.frombuffer(ob[off:off + srcs[0].nbytes].numpy().tobytes(), srcs[0].dtype)
+        assert np.array_equal(bits(got), bits(ref)), (np_, dt, op, n, layout)

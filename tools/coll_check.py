@@ -51,8 +51,9 @@ def upload(dst_ptr, t):
 class Buffers:
     """Source/target pairs in the four residency modes."""
 
-    def __init__(self, hsrc, hdst, nbytes):
+    def __init__(self, hsrc, hdst, nbytes, hh=None):
         self.hsrc, self.hdst, self.nbytes = hsrc, hdst, nbytes
+        self.hh = hh  # (src, dst) in the host symmetric heap (shmem_malloc)
 
     def run(self, mode, src_dev, init_dst, call):
         """Place src (device tensor) and the target's initial bytes, call(dst, src),
@@ -66,6 +67,13 @@ class Buffers:
                 return download(self.hdst, nb)
             call(self.hsrc, self.hsrc)
             return download(self.hsrc, nb)
+        if mode == "hostheap":
+            hs, hd = self.hh
+            ctypes.memmove(hs, src_dev[:nb].cpu().numpy().ctypes.data, nb)
+            ctypes.memmove(hd, init_dst[:nb].cpu().numpy().ctypes.data, nb)
+            call(hd, hs)
+            out = np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(hd)).copy()
+            return torch.from_numpy(out).cuda()
         if mode == "device":
             s = src_dev[:nb].clone()
             d = init_dst[:nb].clone()
@@ -89,6 +97,7 @@ def main():
     hdst = S.shmemx_malloc_device(maxb)
     psync = S.shmem_malloc(8 * 4)
     ctypes.memset(psync, 0, 8 * 4)
+    hh = (S.shmem_malloc(5003 * 16), S.shmem_malloc(5003 * 16))   # host symmetric heap
     S.shmem_barrier_all()
     even = ctypes.c_void_p(0)
     if P >= 3:
@@ -127,10 +136,10 @@ def main():
                     else:
                         exp = outs[idx - 1] if idx else torch.zeros_like(outs[0])
                     zero = torch.zeros_like(ins[idx])
-                    for mode in ("heap", "heap_inplace", "device", "host"):
-                        if mode == "host" and n > 5003:
+                    for mode in ("heap", "heap_inplace", "device", "host", "hostheap"):
+                        if mode in ("host", "hostheap") and n > 5003:
                             continue
-                        got = Buffers(hsrc, hdst, n * es).run(
+                        got = Buffers(hsrc, hdst, n * es, hh).run(
                             mode, ins[idx], zero, lambda d, s: fn(team, d, s, n))
                         mm = L.count_mismatch(exp.data_ptr(), got.data_ptr(), n, es)
                         check(mm == 0, (tname, kind, ty, n, mode, mm))
@@ -175,6 +184,8 @@ def main():
     S.shmemx_free_device(hdst)
     S.shmemx_free_device(hsrc)
     S.shmem_free(psync)
+    S.shmem_free(hh[1])
+    S.shmem_free(hh[0])
     if even.value:
         S.lib().shmem_team_destroy(even)
     sig = {1: "stream", 0: "host"}.get(L.lib().sosx_p2p_signal_mode(), "none")
