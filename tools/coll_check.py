@@ -69,8 +69,10 @@ class Buffers:
             return download(self.hsrc, nb)
         if mode == "hostheap":
             hs, hd = self.hh
-            ctypes.memmove(hs, src_dev[:nb].cpu().numpy().ctypes.data, nb)
-            ctypes.memmove(hd, init_dst[:nb].cpu().numpy().ctypes.data, nb)
+            a_in = src_dev[:nb].cpu().numpy()      # kept alive across the memmoves
+            a_init = init_dst[:nb].cpu().numpy()
+            ctypes.memmove(hs, a_in.ctypes.data, nb)
+            ctypes.memmove(hd, a_init.ctypes.data, nb)
             call(hd, hs)
             out = np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(hd)).copy()
             return torch.from_numpy(out).cuda()
