@@ -241,12 +241,16 @@ def _pinned(torch, raw, offset):
     return buf, buf.data_ptr() + base
 
 
-LAYOUTS = ["aligned", "in_misaligned", "out_misaligned"]
+# every type/op pair on aligned operands (the 16-B-lane path the small host path takes);
+# the misaligned layouts (element lanes, element stores) on a subset of widths
+SMALL_CASES = ([(23, 5, "aligned"), (24, 4, "aligned"), (23, 3, "aligned"), (4, 3, "aligned"),
+                (27, 6, "aligned"), (25, 5, "aligned"), (1, 6, "aligned")]
+               + [(23, 5, "in_misaligned"), (4, 3, "in_misaligned"), (1, 6, "in_misaligned"),
+                  (23, 5, "out_misaligned"), (24, 4, "out_misaligned"), (1, 6, "out_misaligned")])
 
 
-@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("P", [2, 3, 4, 5, 7, 8, 12, 16])
-@pytest.mark.parametrize("dt,op", [(23, 5), (24, 4), (23, 3), (4, 3), (27, 6), (25, 5), (1, 6)])
+@pytest.mark.parametrize("dt,op,layout", SMALL_CASES)
 def test_small_fold_kernel(torch_cuda, P, dt, op, layout):
     """sosx_small_fold (the small host-resident path's one launch): operands, result and
     completion words all in pinned host memory, every PE's own recdbl_sw value (oracle
@@ -293,9 +297,8 @@ def test_small_fold_kernel(torch_cuda, P, dt, op, layout):
             assert np.array_equal(bits(got), bits(ref[me])), (P, dt, op, n, me, layout)
 
 
-@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("P", [2, 3, 4, 5, 8])
-@pytest.mark.parametrize("dt,op", [(23, 5), (24, 4), (23, 3), (4, 6), (27, 6), (25, 5), (1, 5)])
+@pytest.mark.parametrize("dt,op,layout", SMALL_CASES)
 def test_small_ring_kernel(torch_cuda, P, dt, op, layout):
     """sosx_small_ring (the small host-resident path above the crossover): operands,
     result and completion words in pinned host memory; every element equals SOS's ring
@@ -338,9 +341,8 @@ def test_small_ring_kernel(torch_cuda, P, dt, op, layout):
         assert np.array_equal(bits(got), bits(ref[0])), (P, dt, op, n, layout)
 
 
-@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("np_", [1, 2, 3, 5, 8])
-@pytest.mark.parametrize("dt,op", [(23, 5), (24, 5), (4, 5), (27, 5), (25, 5), (1, 5), (24, 4)])
+@pytest.mark.parametrize("dt,op,layout", SMALL_CASES)
 def test_small_linear_kernel(torch_cuda, np_, dt, op, layout):
     """sosx_small_linear (one PE's team scan on the small host-resident path): the
     in-order LINEAR fold of np operands in pinned host memory equals the oracle's
