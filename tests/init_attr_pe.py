@@ -2,7 +2,7 @@
 id handed to the other PEs out of band (a file, as a launcher would broadcast it), then
 shmemx_init_attr -- no TCP bootstrap and no node shared memory, so barriers are RCCL's and
 team agreement (split_strided) goes through the RCCL team-word exchange.  Then it runs
-tools/team_check.py or tools/team_mgmt_check.py (argv[1]) on top of that runtime.
+tests/team_check_pe.py or tools/team_mgmt_check.py (argv[1]) on top of that runtime.
 
 Environment: INIT_ATTR_PE, INIT_ATTR_NPES, INIT_ATTR_UID_FILE.
 """

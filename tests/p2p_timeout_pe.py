@@ -1,6 +1,8 @@
 """Run under tools/oshrun with 2 PEs (p2p transport): PE 1 reaches the reduction 60 s
 late; PE 0, with SHMEMX_P2P_TIMEOUT=3, must end the job with the p2p timeout error
-instead of hanging (tests/test_gpu_multipe.py::test_p2p_wait_is_bounded)."""
+instead of hanging (tests/test_gpu_multipe.py::test_p2p_wait_is_bounded).  With `host`
+as argument the operands are 64 floats in the host symmetric heap, so the call takes the
+small host-resident path and its own bounded waits (test_small_path_wait_is_bounded)."""
 import os
 import sys
 import time
@@ -15,9 +17,11 @@ from sos_amd import shmem as S  # noqa: E402
 def main():
     S.shmem_init()
     me = S.shmem_my_pe()
-    n = 1 << 16
-    src = S.shmemx_malloc_device(n * 4)
-    dst = S.shmemx_malloc_device(n * 4)
+    host = len(sys.argv) > 1 and sys.argv[1] == "host"
+    n = 64 if host else 1 << 16
+    alloc = S.lib().shmem_malloc if host else S.shmemx_malloc_device
+    src = alloc(n * 4)
+    dst = alloc(n * 4)
     S.shmem_barrier_all()
     if me == 1:
         time.sleep(60)

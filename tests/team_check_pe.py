@@ -3,9 +3,14 @@
 Run under tools/oshrun: every PE calls shmem_<T>_<op>_reduce for every schedule
 (auto, ring, recdbl, rechalving, recdbl_direct), several types/ops and sizes, on
 device-heap buffers (shmemx_malloc_device), on plain device buffers, on pageable host
-buffers and on the host symmetric heap (shmem_malloc), in and out of place, over SHMEM_TEAM_WORLD and over a split team.  Each PE
-checks its own result bit for bit against an on-GPU re-evaluation of the schedule's
-element order over all PEs' regenerated inputs.  Prints one line per PE, exit 0 = OK.
+buffers and on the host symmetric heap (shmem_malloc), in and out of place, over
+SHMEM_TEAM_WORLD and over a split team.  Each PE checks its own result bit for bit
+against the CPU oracle (oracle/sos_oracle.c: SOS's ring, src/collectives.c:647-764, or
+recdbl_sw, :850-984, as the schedule resolves) over every member's input regenerated on
+the CPU (oracle_fill, bit-identical to the device generator) -- no library kernel in
+the expected value.  Prints one line per PE, exit 0 = OK.
+
+Test infrastructure: the oracle is the checker only.
 """
 import ctypes
 import os
@@ -17,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from oracle import oracle as O  # noqa: E402
 from sos_amd import _lib as L  # noqa: E402
 from sos_amd import shmem as S  # noqa: E402
 
@@ -26,28 +32,20 @@ ALGS = ["auto", "ring", "recdbl", "rechalving", "recdbl_direct", "recdbl_gather"
 SIZES = [1, 37, 5003, 65536, (1 << 20) + 3]  # 65536: equal ring chunks for P | 65536
 
 
-def expected(dt, opid, dist, seed, members, my_idx, n, es, alg_resolved, pe_of):
+def expected(dt, opid, dist, seed, members, my_idx, n, alg_resolved, pe_of):
+    """This PE's expected target bytes, from the oracle over every member's CPU-generated
+    input: the ring for ring plans, this PE's recdbl_sw value otherwise (rechalving and
+    recdbl_direct evaluate the same tree; for this data, whose ops commute bitwise, every
+    PE's recdbl_sw value is the same)."""
     P = len(members)
-    ins = []
-    for i in range(P):
-        b = torch.empty(n * es, dtype=torch.uint8, device="cuda")
-        L.fill(dt, dist, seed, pe_of(i), b.data_ptr(), n)
-        ins.append(b)
-    exp = torch.empty(n * es, dtype=torch.uint8, device="cuda")
+    ins = [O.fill(dt, dist, seed, pe_of(i), n) for i in range(P)]
     if P == 1:
-        exp.copy_(ins[0])
+        out = ins[0]
     elif alg_resolved == L.ALGS["ring"]:
-        q, r = divmod(n, P)
-        for c in range(P):
-            cnt = q + (c < r)
-            first = c * cnt if c < r else c * cnt + r
-            if cnt:
-                L.fold(opid, dt, L.ORDER_LINEAR, exp.data_ptr() + first * es,
-                       [ins[(c + k) % P].data_ptr() + first * es for k in range(P)], cnt)
+        out = O.ring(opid, dt, ins)[my_idx]
     else:
-        L.fold(opid, dt, L.ORDER_TREE, exp.data_ptr(), [x.data_ptr() for x in ins], n)
-    torch.cuda.synchronize()
-    return exp
+        out = O.recdbl(opid, dt, ins)[my_idx]
+    return torch.from_numpy(np.frombuffer(out.tobytes(), np.uint8).copy()).cuda()
 
 
 def main():
@@ -82,6 +80,7 @@ def main():
                     continue
                 seed = zlib.crc32(f"{alg}/{tname}/{oname}/{n}".encode())
                 resolved = S.lib().sosx_resolve_alg(L.ALGS[alg], n * es, 16384)
+                exp = None
                 for mode in ("heap", "heap_inplace", "device", "host", "hostheap"):
                     # host operands up to 64Ki elements (the small path's ring sizes) at
                     # P <= 4; at P = 8 on one GPU those calls are staged and slow
@@ -117,7 +116,8 @@ def main():
                         tmp = torch.from_numpy(h_out.copy()).cuda()
                         torch.cuda.synchronize()
                         out = tmp.data_ptr()
-                    exp = expected(dt, opid, dist, seed, list(range(P)), me, n, es, resolved, lambda i: i)
+                    if exp is None:
+                        exp = expected(dt, opid, dist, seed, list(range(P)), me, n, resolved, lambda i: i)
                     mm = L.count_mismatch(exp.data_ptr(), out, n, es)
                     checks += 1
                     if mm:
@@ -128,7 +128,7 @@ def main():
                     torch.cuda.synchronize()
                     fn(even.value, hdst, hsrc, n)
                     m = (P + 1) // 2
-                    exp = expected(dt, opid, dist, seed, list(range(m)), me // 2, n, es, resolved,
+                    exp = expected(dt, opid, dist, seed, list(range(m)), me // 2, n, resolved,
                                    lambda i: 2 * i)
                     mm = L.count_mismatch(exp.data_ptr(), hdst, n, es)
                     checks += 1

@@ -68,7 +68,7 @@ def _used_fake(r, np_):
 @pytest.mark.parametrize("np_", [2, 3, 4])
 def test_team_check_rccl_executor(np_):
     """Every schedule, 8 type/op pairs, heap / device / host buffers, in place, a split team."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900)
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900)
     _ok(r, np_)
 
 
@@ -76,7 +76,7 @@ def test_team_check_rccl_executor(np_):
 def test_team_check_rccl_native_allgather(np_):
     """SHMEMX_RCCL_ALLGATHER=1: equal-chunk allgather rounds of world-team plans go through
     ncclAllGather (counted by the stand-in); every check stays bit-exact."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
                SHMEMX_RCCL_ALLGATHER="1")
     _ok(r, np_)
     ag = {int(rk): int(a) for rk, a in
@@ -132,9 +132,9 @@ def test_api_sweep_rccl_native_allreduce(np_):
 
 @pytest.mark.parametrize("np_", [2, 4])
 def test_team_check_rccl_native_allreduce(np_):
-    """The same switch under tools/team_check.py: world-team integer calls through
+    """The same switch under tests/team_check_pe.py: world-team integer calls through
     ncclAllReduce, split-team calls (not world-shaped) on their schedules, all bit-exact."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
                SHMEMX_RCCL_ALLREDUCE="1")
     _ok(r, np_)
 
@@ -226,7 +226,7 @@ def test_bench_preflight_drops_a_hanging_transport():
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0, res["check"]
 
 
-@pytest.mark.parametrize("script", ["team_check.py", "team_mgmt_check.py"])
+@pytest.mark.parametrize("script", ["tests/team_check_pe.py", "tools/team_mgmt_check.py"])
 def test_init_attr_multi_pe(tmp_path, script, np_=3):
     """shmemx_init_attr across 3 processes (unique id passed out of band, no bootstrap hub):
     RCCL barriers and the RCCL team-word agreement under the team checkers."""
@@ -239,7 +239,7 @@ def test_init_attr_multi_pe(tmp_path, script, np_=3):
                     "INIT_ATTR_UID_FILE": str(tmp_path / "uid")})
         procs.append(subprocess.Popen(
             [sys.executable, os.path.join(ROOT, "tests", "init_attr_pe.py"),
-             os.path.join(ROOT, "tools", script)],
+             os.path.join(ROOT, script)],
             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     outs = []
     try:

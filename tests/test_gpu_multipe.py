@@ -63,7 +63,7 @@ def test_team_check(np_, signal):
     """Every schedule across np_ PE processes, with the p2p transport's counters moved by
     stream-ordered device signals (the default) or by the host every round
     (SHMEMX_P2P_SIGNAL=host)."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
                extra_env={"SHMEMX_P2P_SIGNAL": signal})
     # PEs print concurrently, so lines may interleave: count the reports, not lines
     ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+), small-path calls (\d+)\)",
@@ -79,7 +79,7 @@ def test_team_check(np_, signal):
 def test_team_check_small_path_off(np_):
     """SHMEMX_SMALL_HOST=0: the same checks with every host-resident call on the general
     (staged) path -- both paths give the oracle's bits."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
                extra_env={"SHMEMX_SMALL_HOST": "0"})
     ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal \w+, small-path calls (\d+)\)", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
@@ -109,6 +109,19 @@ def test_p2p_wait_is_bounded(signal):
                extra_env={"SHMEMX_P2P_TIMEOUT": "3", "SHMEMX_P2P_SIGNAL": signal})
     assert r.returncode != 0, r.stdout
     assert "p2p transport: timed out" in r.stderr, r.stderr[-2000:]
+    assert "reduction returned" not in r.stdout
+    assert time.monotonic() - t0 < 55, "the job outlived the late PE's sleep"
+
+
+def test_small_path_wait_is_bounded():
+    """The same late PE with host-heap operands: the call takes the small host-resident
+    path (node shared memory), whose waits for a peer's operand are bounded by
+    SHMEMX_P2P_TIMEOUT too."""
+    t0 = time.monotonic()
+    r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "p2p_timeout_pe.py"), "host"],
+               timeout=150, extra_env={"SHMEMX_P2P_TIMEOUT": "3"})
+    assert r.returncode != 0, r.stdout
+    assert "small host-resident reduction: timed out" in r.stderr, r.stderr[-2000:]
     assert "reduction returned" not in r.stdout
     assert time.monotonic() - t0 < 55, "the job outlived the late PE's sleep"
 
@@ -237,7 +250,7 @@ def test_ipc_heap_sizes_with_bit31(heap):
 @pytest.mark.parametrize("np_,signal", [(2, "host"), (3, "host"), (8, "host"), (3, "stream")])
 def test_team_check_host_stripes(np_, signal):
     """Host-resident ring reductions pipelined in stripes (striped_host_ring): with 256-B
-    chunk slices the host-buffer calls of tools/team_check.py run as many stripes plus
+    chunk slices the host-buffer calls of tests/team_check_pe.py run as many stripes plus
     the n mod P remainder stripe (p2p stripes only when SHMEMX_HOST_STRIPE_BYTES is set),
     bit for bit against the schedule-order fold."""
     env = {"SHMEMX_HOST_STRIPE_BYTES": "256", "SHMEMX_P2P_SIGNAL": signal}
@@ -245,7 +258,7 @@ def test_team_check_host_stripes(np_, signal):
         # eight processes' default hardware queues oversubscribe one GPU (DESIGN §7,
         # profiles/r2_onegpu_hw_queue_oversubscription.txt): 72 s with 4 queues each
         env["GPU_MAX_HW_QUEUES"] = "1"
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "team_check.py")], timeout=900,
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
                extra_env=env)
     ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)[,)]", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \

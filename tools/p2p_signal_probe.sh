@@ -15,8 +15,8 @@ run() {  # name seconds cmd...
     tail -n 4 "gpurun_out/$name.out"
     [ $rc -eq 0 ] || exit $rc
 }
-SHMEMX_P2P_SIGNAL=stream run tc2 200 python tools/oshrun -np 2 --timeout 180 python tools/team_check.py
-SHMEMX_P2P_SIGNAL=stream run tc3 200 python tools/oshrun -np 3 --timeout 180 python tools/team_check.py
+SHMEMX_P2P_SIGNAL=stream run tc2 200 python tools/oshrun -np 2 --timeout 180 python tests/team_check_pe.py
+SHMEMX_P2P_SIGNAL=stream run tc3 200 python tools/oshrun -np 3 --timeout 180 python tests/team_check_pe.py
 for P in 2 4 8; do
     for m in stream host; do
         SHMEMX_P2P_SIGNAL=$m run lat_${m}_$P 200 python tools/oshrun -np $P --timeout 180 python tools/latency_check.py
