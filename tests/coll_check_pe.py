@@ -4,11 +4,13 @@ Run under tools/oshrun: every PE calls shmemx_<T>_sum_{inscan,exscan},
 shmem_<T>_broadcast, shmem_broadcastmem and the active-set shmem_broadcast32/64 on
 device-heap buffers (shmemx_malloc_device), plain device buffers and host buffers, in
 and out of place, over SHMEM_TEAM_WORLD and over an even-PE split team.  Scan results
-are checked bit for bit against a single-launch prefix (sosx_prefix) over all PEs'
-regenerated inputs -- the element order of SOS scan_ring (src/collectives.c:1111-1209);
+are checked bit for bit against the CPU oracle's SOS scan_ring (oracle.scan,
+src/collectives.c:1111-1209) over every member's input regenerated on the CPU;
 broadcast results against the root's regenerated input, with the root's target
 checked for SOS's copy / no-copy rule (src/collectives_c.c4:342-429).
 Prints one line per PE, exit 0 = OK.
+
+Test infrastructure: the oracle is the checker only.
 """
 import ctypes
 import os
@@ -20,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from oracle import oracle as O  # noqa: E402
 from sos_amd import _lib as L  # noqa: E402
 from sos_amd import shmem as S  # noqa: E402
 
@@ -129,20 +132,16 @@ def main():
                 for kind in ("inscan", "exscan"):
                     fn = getattr(S, f"shmemx_{ty}_sum_{kind}")
                     seed = zlib.crc32(f"{tname}/{ty}/{n}/{kind}".encode())
-                    ins = [gen(dt, seed, members[i], n, es) for i in range(m)]
-                    outs = [torch.empty_like(x) for x in ins]
-                    L.prefix("sum", dt, [o.data_ptr() for o in outs], [x.data_ptr() for x in ins], n)
-                    torch.cuda.synchronize()
-                    if kind == "inscan":
-                        exp = outs[idx]
-                    else:
-                        exp = outs[idx - 1] if idx else torch.zeros_like(outs[0])
-                    zero = torch.zeros_like(ins[idx])
+                    mine = gen(dt, seed, members[idx], n, es)
+                    cpu_ins = [O.fill(dt, L.DIST_UNIFORM, seed, members[i], n) for i in range(m)]
+                    ref = O.scan(L.op_id("sum"), dt, cpu_ins, kind == "exscan")[idx]
+                    exp = torch.from_numpy(np.frombuffer(ref.tobytes(), np.uint8).copy()).cuda()
+                    zero = torch.zeros_like(mine)
                     for mode in ("heap", "heap_inplace", "device", "host", "hostheap"):
                         if mode in ("host", "hostheap") and n > 5003:
                             continue
                         got = Buffers(hsrc, hdst, n * es, hh).run(
-                            mode, ins[idx], zero, lambda d, s: fn(team, d, s, n))
+                            mode, mine, zero, lambda d, s: fn(team, d, s, n))
                         mm = L.count_mismatch(exp.data_ptr(), got.data_ptr(), n, es)
                         check(mm == 0, (tname, kind, ty, n, mode, mm))
         # ---- typed / mem broadcasts -----------------------------------------------------

@@ -88,7 +88,7 @@ def test_team_check_rccl_native_allgather(np_):
 @pytest.mark.parametrize("np_", [3])
 def test_coll_check_rccl_executor(np_):
     """Scans and broadcasts over the RCCL executor."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "coll_check.py")], timeout=600)
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "coll_check_pe.py")], timeout=600)
     _ok(r, np_)
 
 

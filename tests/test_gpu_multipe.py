@@ -90,9 +90,9 @@ def test_team_check_small_path_off(np_):
 @pytest.mark.parametrize("np_,signal", [(2, "host"), (3, "host"), (4, "host"), (8, "host"),
                                          (3, "stream"), (8, "stream")])
 def test_coll_check(np_, signal):
-    """Scans and broadcasts through the public API (tools/coll_check.py), p2p counters
+    """Scans and broadcasts through the public API (tests/coll_check_pe.py), p2p counters
     moved by the host or by stream-ordered device signals."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tools", "coll_check.py")], timeout=900,
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "coll_check_pe.py")], timeout=900,
                extra_env={"SHMEMX_P2P_SIGNAL": signal})
     ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)[,)]", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
