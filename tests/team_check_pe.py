@@ -145,6 +145,45 @@ def main():
                     checks += 1
                     if mm:
                         bad.append((alg, tname, oname, n, "even_team_hostheap", mm))
+    # Per-PE perspective values across real processes: fp min/max/sum with +-0 ties and a
+    # NaN whose payload differs per PE, under the schedules that give every PE its own
+    # recdbl_sw value (recdbl, recdbl_gather, AUTO below the crossover); the PEs'
+    # expected targets genuinely differ (x86 keeps the first NaN operand, the ternary
+    # min/max returns the second operand on ties).
+    for alg in ("recdbl", "recdbl_gather", "auto"):
+        S.shmemx_set_reduce_algorithm(L.ALGS[alg])
+        for tname, oname in (("double", "max"), ("float", "min"), ("double", "sum")):
+            dt, opid = L.dtype_id(tname), L.op_id(oname)
+            es = L.dtype_size(dt)
+            fn = getattr(S, f"shmem_{tname}_{oname}_reduce")
+            for n in (2, 37, 1001):
+                seed = zlib.crc32(f"persp/{alg}/{tname}/{oname}/{n}".encode())
+                ins = [_perspective(O.fill(dt, L.DIST_UNIFORM, seed, pe, n), pe) for pe in range(P)]
+                exp_np = O.recdbl(opid, dt, ins)[me]
+                exp = torch.from_numpy(np.frombuffer(exp_np.tobytes(), np.uint8).copy()).cuda()
+                mine = np.frombuffer(ins[me].tobytes(), np.uint8).copy()
+                for mode in ("heap", "hostheap", "host"):
+                    if mode == "heap":
+                        _hip_copy(hsrc, mine.ctypes.data, n * es)
+                        fn(world, hdst, hsrc, n)
+                        out = hdst
+                    elif mode == "hostheap":
+                        ctypes.memmove(hh_in, mine.ctypes.data, n * es)
+                        fn(world, hh_out, hh_in, n)
+                        h_out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * es)).from_address(hh_out))
+                        tmp = torch.from_numpy(h_out.copy()).cuda()
+                        out = tmp.data_ptr()
+                    else:
+                        h_out = np.zeros_like(mine)
+                        fn(world, h_out.ctypes.data, mine.ctypes.data, n)
+                        tmp = torch.from_numpy(h_out).cuda()
+                        out = tmp.data_ptr()
+                    torch.cuda.synchronize()
+                    mm = L.count_mismatch(exp.data_ptr(), out, n, es)
+                    checks += 1
+                    if mm:
+                        bad.append(("perspective", alg, tname, oname, n, mode, mm))
+    S.shmemx_set_reduce_algorithm(L.ALGS["auto"])
     S.shmem_barrier_all()
     S.shmemx_free_device(hdst)
     S.shmemx_free_device(hsrc)
@@ -160,6 +199,16 @@ def main():
         return 1
     print(f"PE {me}/{P}: {checks} checks OK (p2p signal {sig}, small-path calls {small})", flush=True)
     return 0
+
+
+def _perspective(a, pe):
+    """Element 0 a signed zero by PE parity, element 1 a NaN with payload pe + 1."""
+    a = a.copy()
+    ity = np.uint32 if a.dtype == np.float32 else np.uint64
+    a[0] = -0.0 if pe % 2 else 0.0
+    if a.size > 1:
+        a.view(ity)[1] = (ity(0x7FC00000) if ity is np.uint32 else ity(0x7FF8000000000000)) | ity(pe + 1)
+    return a
 
 
 def _download(ptr, nbytes):

@@ -25,6 +25,12 @@ def oshrun(np_, cmd, timeout=600, extra_env=None):
         env.pop(k, None)
     env.update({"SHMEMX_TRANSPORT": "p2p", "SHMEMX_DEVICE_HEAP_SIZE": "256M",
                 "SHMEMX_STAGE_BYTES": "64M", "SHMEMX_DEVICE": "0", "PYTHONPATH": ROOT})
+    if np_ >= 8:
+        # eight PE processes on the box's one GPU, next to this pytest process's own
+        # queues, oversubscribe the device's hardware queues and every call then waits on
+        # queue time-slicing: one hardware queue per PE process
+        # (the full suite measured test_coll_check[8] at 110 s with the default, 4 s alone)
+        env["GPU_MAX_HW_QUEUES"] = "1"
     env.update(extra_env or {})
     return subprocess.run([sys.executable, OSHRUN, "-np", str(np_), "--timeout", str(timeout - 30),
                            *cmd], capture_output=True, text=True, timeout=timeout, env=env)
@@ -252,12 +258,8 @@ def test_team_check_host_stripes(np_, signal):
     """Host-resident ring reductions pipelined in stripes (striped_host_ring): with 256-B
     chunk slices the host-buffer calls of tests/team_check_pe.py run as many stripes plus
     the n mod P remainder stripe (p2p stripes only when SHMEMX_HOST_STRIPE_BYTES is set),
-    bit for bit against the schedule-order fold."""
+    bit for bit against the CPU oracle."""
     env = {"SHMEMX_HOST_STRIPE_BYTES": "256", "SHMEMX_P2P_SIGNAL": signal}
-    if np_ >= 8:
-        # eight processes' default hardware queues oversubscribe one GPU (DESIGN §7,
-        # profiles/r2_onegpu_hw_queue_oversubscription.txt): 72 s with 4 queues each
-        env["GPU_MAX_HW_QUEUES"] = "1"
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
                extra_env=env)
     ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)[,)]", r.stdout)
