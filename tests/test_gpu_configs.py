@@ -8,7 +8,8 @@ src/shmem_internal_op.h:305-339, and the ring schedule, src/collectives.c:647-76
   config #4  float sum over 8 PEs, nreduce = 64Mi (single-GPU loopback team: the same
              per-PE ring plan and fold kernels the RCCL executor runs)
   config #5  int / double / complexd x min / max / prod (complexd: prod, sum) at the
-             sweep's largest size, nreduce = 256Mi
+             sweep's largest size, nreduce = 256Mi, and through the team schedules at
+             P = 2 / 4 / 8 for nreduce = 1Ki, 64Ki, 4Mi
 
 Inputs are the SURVEY 8(d) synthetic streams, generated on the GPU (sosx_fill) and on the
 host (oracle fill) -- test_fill_matches_oracle pins that the two are identical.
@@ -79,3 +80,29 @@ def test_config4_float_sum_8pes_64mi(torch_cuda, sos, oracle):
     for p in range(P):
         got = dst[p].cpu().numpy()
         assert np.array_equal(got, np.frombuffer(ref[p].tobytes(), np.uint8)), p
+
+
+@pytest.mark.parametrize("P,n", [(2, 1024), (2, 65536), (2, 4 * Mi), (4, 1024), (4, 65536), (4, 4 * Mi),
+                                 (8, 1024), (8, 65536), (8, 4 * Mi)])
+@pytest.mark.parametrize("dt,op", [(4, 3), (4, 4), (4, 6), (24, 3), (24, 4), (24, 6), (27, 6), (27, 5)])
+def test_config5_sweep_team(torch_cuda, sos, oracle, P, n, dt, op):
+    """Config #5 at P = 2/4/8: int / double / complexd x min / max / prod
+    (complexd: prod, sum) through the schedule SOS AUTO picks at that size -- recdbl_sw
+    below the 16 KiB crossover, the ring above it -- every PE bit for bit against the
+    oracle's schedule over the CPU-regenerated inputs (loopback team on one GPU: the same
+    per-PE plans and kernels the transports run)."""
+    from sos_amd import shmem as S
+    torch = torch_cuda
+    dist = 1 if op == 6 else 0
+    es = sos.dtype_size(dt)
+    alg = "recdbl" if n * es < 16384 else "ring"
+    src = [dev_fill(torch, sos, dt, dist, p, n) for p in range(P)]
+    dst = [torch.empty_like(t) for t in src]
+    S.loopback_allreduce(alg, op, dt, [t.data_ptr() for t in src], [t.data_ptr() for t in dst], n)
+    torch.cuda.synchronize()
+    del src
+    ins = [oracle.fill(dt, dist, SEED, p, n) for p in range(P)]
+    ref = oracle.ring(op, dt, ins) if alg == "ring" else oracle.recdbl(op, dt, ins)
+    for p in range(P):
+        got = dst[p].cpu().numpy()
+        assert np.array_equal(got, np.frombuffer(ref[p].tobytes(), np.uint8)), (alg, p)
