@@ -8,11 +8,15 @@
 //   1. each PE copies its source into its slot of the node shared segment (host
 //      memory every PE maps, registered with HIP on every GPU: fine-grained, mapped);
 //   2. host flags (release/acquire) publish the slot to the team;
-//   3. ONE kernel per PE (sosx_small_fold) reads all P slots in place over the host
-//      link and writes the PE's result -- the recdbl_gather evaluation: every PE
-//      computes ITS OWN recdbl_sw expression (the extra-PE folds, then the TREE over the
-//      leaves permuted by my_idx; see plan.cpp build_recdbl_gather), bit for bit, +-0
-//      ties and NaN payloads included;
+//   3. ONE kernel per PE (small.hip) reads all P slots in place over the host link and
+//      writes the PE's result, as the schedule SOS would run prescribes:
+//      - recdbl_sw (AUTO below the crossover, sosx_small_fold): every PE computes ITS OWN
+//        recdbl_sw expression (the extra-PE folds, then the TREE over the leaves
+//        permuted by my_idx; see plan.cpp build_recdbl_gather), bit for bit, +-0 ties
+//        and NaN payloads included;
+//      - the ring (AUTO above it, sosx_small_ring): chunk c folded from PE c, every
+//        chunk evaluated by every PE (the allgather's result);
+//      - the team scans (sosx_small_linear): the in-order prefix of the team's sources;
 //   4. the result lands in `target` directly when it is in the (device-mapped) host
 //      symmetric heap, else in a pinned slot copied out; the host learns that the kernel
 //      finished from per-workgroup completion words in pinned memory, not from a
