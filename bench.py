@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-host", action="store_true", help="skip the host-resident leg")
+    p.add_argument("--no-small", action="store_true",
+                   help="N > 1: skip the small-message leg (library vs SOS's CPU path)")
     p.add_argument("--no-adjacent", action="store_true",
                    help="skip the scan/broadcast legs (prefix kernel at N=1, team calls at N>1)")
     p.add_argument("--team", action="store_true",

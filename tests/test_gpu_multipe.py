@@ -198,6 +198,12 @@ def test_bench_team_leg(np_):
         assert curve[-1]["bitwise_mismatches_all_ranks"] == 0
     # the local combine on every PE at once (the HBM side of the curve)
     assert res["local_combine_all_pes"]["value_GiBs"] > 0, res["local_combine_all_pes"]
+    # small / medium calls beside SOS's CPU path, host-heap results equal to the CPU's
+    small = res["small_messages"]["rows"]
+    assert [r["nreduce"] for r in small] == [1, 1024, 16384, 65536]
+    for row in small:
+        assert row["host_us"] > 0 and row["device_us"] > 0 and row["cpu_us"] > 0, row
+        assert row["host_bitwise_mismatches_vs_cpu_all_ranks"] == 0, row
     # SOS's ring on np_ host processes beside the line, equal to the GPU ring byte for byte
     cpu = res["cpu_ring_baseline"]
     assert cpu["cores"] == np_ and cpu["value"] > 0 and cpu["kind"] == "port", cpu

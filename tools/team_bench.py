@@ -253,6 +253,9 @@ def main(args, torch, pmc=None):
 
     local_leg = local_combine(args, torch, dist, L, dt, es, n, src, dst, stream, world)
 
+    small = {} if (getattr(args, "no_small", False) or getattr(args, "no_cpu", False)) else \
+        small_messages(args, torch, dist, L, S, team, rank, world, stream)
+
     # HBM traffic of the fold kernel: rank 0 runs bench.py's PMC passes (rocprofv3 --pmc
     # FETCH_SIZE, then WRITE_SIZE) over a one-process child launching the same kernel at
     # this call's shape (P inputs of n/P elements) on its GPU; the other ranks wait
@@ -354,6 +357,8 @@ def main(args, torch, pmc=None):
         res["adjacent_collectives"] = adjacent
     if cpu_ring:
         res["cpu_ring_baseline"] = cpu_ring
+    if small:
+        res["small_messages"] = small
     if rank == 0:
         print(json.dumps(res), flush=True)
     dist.barrier()
@@ -517,6 +522,125 @@ def cpu_ring_baseline(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed
                r["bitwise_mismatches_vs_gpu_ring_all_ranks"] for r in rows),
            "rows": rows}
     return out
+
+
+def small_messages(args, torch, dist, L, S, team, rank, world, stream):
+    """Small and medium shmem_float_sum_reduce(SHMEM_TEAM_WORLD) calls under SOS AUTO,
+    microseconds per call (max over ranks), beside SOS's own CPU path on the same
+    processes:
+      host   : operands in the host symmetric heap (shmem_malloc), SOS's own case -- the
+               small host-resident path (one kernel per PE over node shared memory);
+      device : operands in the device symmetric heap (shmemx_malloc_device), on the
+               library's default transport;
+      cpu    : SOS AUTO on the CPU -- recdbl_sw below 16 KiB, the ring above
+               (oracle_pe_recdbl / oracle_pe_ring, src/collectives.c:850-984, :647-764),
+               one pinned physical core per PE, memcpy puts over /dev/shm.
+    At every size the host-heap result is compared byte for byte with the CPU result.
+    Test infrastructure in the timed-baseline role only."""
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    from oracle import oracle as O
+    sizes = [1, 1024, 16384, 65536]          # fp32: 4 B .. 256 KiB
+    nmax, dt, opid, es = max(sizes), L.dtype_id("float"), L.op_id("sum"), 4
+    seed = 0x5A11
+    S.shmemx_set_reduce_algorithm(L.ALGS["auto"])
+    hsrc, hdst = S.lib().shmem_malloc(nmax * es), S.lib().shmem_malloc(nmax * es)
+    dsrc, ddst = S.shmemx_malloc_device(nmax * es), S.shmemx_malloc_device(nmax * es)
+    if not (hsrc and hdst and dsrc and ddst):
+        return {"skipped": "symmetric allocation failed"}
+    mine = O.fill(dt, L.DIST_UNIFORM, seed, rank, nmax)
+    np.ctypeslib.as_array((ctypes_u8 * (nmax * es)).from_address(hsrc))[:] = mine.view(np.uint8)
+    L.fill(dt, L.DIST_UNIFORM, seed, rank, dsrc, nmax, 0, stream)
+    torch.cuda.synchronize()
+
+    def timed(call, reps):
+        for _ in range(10):
+            call()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            call()
+        t1 = time.perf_counter()
+        el = torch.tensor([t1 - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return el.item() / reps
+
+    small_before = S.lib().sosx_small_path_calls()
+    rows = []
+    for n in sizes:
+        reps = 200 if n <= 16384 else 50
+        th = timed(lambda: S.shmem_float_sum_reduce(team, hdst, hsrc, n), reps)
+        td = timed(lambda: S.shmem_float_sum_reduce(team, ddst, dsrc, n), reps)
+        rows.append({"nreduce": n, "bytes": n * es,
+                     "schedule": "recdbl_sw" if n * es < 16384 else "ring",
+                     "host_us": round(th * 1e6, 2), "device_us": round(td * 1e6, 2)})
+    small_calls = S.lib().sosx_small_path_calls() - small_before
+
+    # SOS's CPU path on the same ranks, pinned one physical core each
+    allowed = sorted(os.sched_getaffinity(0))
+    primaries = []
+    for c in allowed:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                first = int(f.read().replace("-", ",").split(",")[0])
+        except (OSError, ValueError):
+            first = c
+        if first == c or first not in allowed:
+            primaries.append(c)
+    path = f"/dev/shm/sosx_small_{os.environ.get('MASTER_PORT', '0')}_{world}"
+    ring = None
+    try:
+        if rank == 0:
+            if os.path.exists(path):
+                os.unlink(path)
+            ring = O.PeRing(path, world, 0, nmax, dt, create=True, alg="recdbl")
+        dist.barrier()
+        if rank != 0:
+            ring = O.PeRing(path, world, rank, nmax, dt, create=False, alg="recdbl")
+        dist.barrier()
+        if rank == 0:
+            os.unlink(path)
+        for row in rows:
+            n = row["nreduce"]
+            ring.count = n
+            ring.alg = O.PeRing.ALGS["recdbl" if n * es < 16384 else "ring"]
+            os.sched_setaffinity(0, {primaries[rank % len(primaries)]})
+            reps = 2000 if n <= 16384 else 200
+            ring.time(opid, mine, max(10, reps // 10))
+            t = ring.time(opid, mine, reps) / reps
+            ring.barrier()
+            os.sched_setaffinity(0, set(allowed))
+            el = torch.tensor([t], dtype=torch.float64)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            row["cpu_us"] = round(el.item() * 1e6, 2)
+            # the library's host-heap result for these inputs vs SOS's CPU result
+            S.shmem_float_sum_reduce(team, hdst, hsrc, n)
+            got = np.ctypeslib.as_array((ctypes_u8 * (n * es)).from_address(hdst)).copy()
+            exp = ring.target().view(np.uint8)[:n * es].copy()
+            mm = torch.tensor([int(np.count_nonzero(got.view(np.uint32) != exp.view(np.uint32)))],
+                              dtype=torch.int64)
+            dist.all_reduce(mm, op=dist.ReduceOp.SUM)
+            row["host_bitwise_mismatches_vs_cpu_all_ranks"] = int(mm.item())
+            ring.barrier()
+    finally:
+        if ring is not None:
+            ring.close()
+        os.sched_setaffinity(0, set(allowed))
+    S.shmemx_free_device(ddst)
+    S.shmemx_free_device(dsrc)
+    S.lib().shmem_free(hdst)
+    S.lib().shmem_free(hsrc)
+    if rank == 0:
+        for r in rows:
+            log(f"[small] n={r['nreduce']} host {r['host_us']} us, device {r['device_us']} us, "
+                f"SOS CPU {r['cpu_us']} us, mismatches {r['host_bitwise_mismatches_vs_cpu_all_ranks']}")
+    return {"op": "float sum", "algorithm": "auto", "rows": rows,
+            "small_path_calls_rank0_side": int(small_calls),
+            "note": "us per call, max over ranks; host = host symmetric heap (small host-resident "
+                    "path), device = device symmetric heap (default transport), cpu = SOS AUTO "
+                    "on the CPU (recdbl_sw < 16 KiB, ring above), one pinned core per PE"}
 
 
 def host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
