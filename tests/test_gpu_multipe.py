@@ -93,6 +93,18 @@ def test_team_check_small_path_off(np_):
     assert all(int(c) == 0 for _, c in ok), ok
 
 
+def test_team_check_small_path_bytes():
+    """SHMEMX_SMALL_HOST_BYTES=4096: host operands up to 4 KiB take the small path, larger
+    ones the staged path, in the same job -- every result the oracle's bits, and the small
+    path did run."""
+    r = oshrun(3, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
+               extra_env={"SHMEMX_SMALL_HOST_BYTES": "4096"})
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal \w+, small-path calls (\d+)\)", r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == [0, 1, 2], \
+        r.stdout + r.stderr[-3000:]
+    assert all(int(c) > 0 for _, c in ok), ok
+
+
 @pytest.mark.parametrize("np_,signal", [(2, "host"), (3, "host"), (4, "host"), (8, "host"),
                                          (3, "stream"), (8, "stream")])
 def test_coll_check(np_, signal):
