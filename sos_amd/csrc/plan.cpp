@@ -51,7 +51,9 @@ int build_direct(int alg, int P, int me, uint64_t count, uint64_t ts, unsigned s
     // Scratch slot for each peer's copy of my chunk, 16-B congruent with my DST chunk.
     // Consecutive slots sit chunk + 1 KiB apart (for 1 KiB-multiple chunks): the P-input
     // fold over them streams ~2 % faster than with 256-B skews (tools/fold_layout_probe.py
-    // on two boxes, profiles/r3_fold_layout_probe.json: 5.96-5.98 vs 5.83-5.84 TB/s).
+    // on two boxes, profiles/r3_fold_layout_probe.json: 5.96-5.98 vs 5.83-5.84 TB/s); in
+    // the 8-PE loopback ring the fold's mean moved 102.3 -> 101.7 us, inside its 94-110 us
+    // per-PE spread (the caller's own source and target placement dominates there).
     const uint64_t mis = (dst_mis + first_me * ts) & 15;
     const uint64_t stride = round_up(my_bytes + 16, 1024);
     auto slot = [&](int peer) { return (uint64_t)((peer - me - 1 + P) % P) * stride + mis; };
