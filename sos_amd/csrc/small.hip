@@ -21,17 +21,22 @@ namespace sos {
 // in first, src/collectives.c:905-926) or leaf[y] alone; the leaves are then reduced by
 // the butterfly's tree (:932-963, fold_elem TREE).  P2 = 0: a runtime leaf count of 16..64
 // (several PEs per GPU), walked with the binary-counter stack of k_fold_dyn.
-struct SmallFoldArgs {
-    const void *leaf[SOSX_MAX_FOLD];
-    const void *extra[SOSX_MAX_FOLD];  // null: the leaf has no extra PE
+// MAXP = 8 for the P2 <= 8 kernels (one PE per GPU on a node): 150 B of kernel
+// arguments instead of 1 KiB, which the host launch call copies every time
+// (SOSX_SMALL_TRACE measured the launch call at 3.0 us with the 1 KiB block).
+template <int MAXP> struct SmallFoldArgsT {
+    const void *leaf[MAXP];
+    const void *extra[MAXP];           // null: the leaf has no extra PE
     uint32_t *flags;                   // one word per workgroup
     uint32_t seq;
     int p2;
     int vec_out;                       // out is 16-B aligned: vector stores
 };
+using SmallFoldArgs = SmallFoldArgsT<SOSX_MAX_FOLD>;
+using SmallFoldArgs8 = SmallFoldArgsT<8>;
 
-template <class T, class OP, int P2>
-__device__ __forceinline__ T small_tree_elem(const SmallFoldArgs &a, size_t i)
+template <class T, class OP, int P2, class A>
+__device__ __forceinline__ T small_tree_elem(const A &a, size_t i)
 {
     if constexpr (P2 > 0) {
         T v[P2], x[P2];
@@ -86,8 +91,8 @@ __device__ __forceinline__ void store_pack(T *out, size_t i0, const Pack<T> &r, 
 // VEC: lane L handles elements [L*V, L*V + V) as 16-B vectors (every leaf/extra 16-B
 // aligned); the last, partial vector goes element by element.  Otherwise one element per
 // lane.
-template <class T, class OP, int P2, bool VEC>
-__global__ __launch_bounds__(kThreads) void k_small_fold(T *out, SmallFoldArgs a, size_t n)
+template <class T, class OP, int P2, bool VEC, class A>
+__global__ __launch_bounds__(kThreads) void k_small_fold(T *out, A a, size_t n)
 {
     const size_t lane = (size_t)blockIdx.x * kThreads + threadIdx.x;
     if constexpr (VEC && P2 > 0) {
@@ -113,10 +118,10 @@ __global__ __launch_bounds__(kThreads) void k_small_fold(T *out, SmallFoldArgs a
             }
             store_pack<T>(out, i0, r, a.vec_out != 0);
         } else {
-            for (size_t i = i0; i < n; ++i) out[i] = small_tree_elem<T, OP, P2>(a, i);
+            for (size_t i = i0; i < n; ++i) out[i] = small_tree_elem<T, OP, P2, A>(a, i);
         }
     } else {
-        if (lane < n) out[lane] = small_tree_elem<T, OP, P2>(a, lane);
+        if (lane < n) out[lane] = small_tree_elem<T, OP, P2, A>(a, lane);
     }
     signal_done(a.flags, a.seq);
 }
@@ -194,15 +199,27 @@ struct SmallFoldFn {
     template <class T, class OP>
     static int run(void *out, const SmallFoldArgs *a, size_t n, bool vec, unsigned blocks, hipStream_t st)
     {
+        SmallFoldArgs8 a8;
+        memset(&a8, 0, sizeof(a8));
+        if (a->p2 <= 8) {
+            for (int y = 0; y < a->p2; ++y) {
+                a8.leaf[y] = a->leaf[y];
+                a8.extra[y] = a->extra[y];
+            }
+            a8.flags = a->flags;
+            a8.seq = a->seq;
+            a8.p2 = a->p2;
+            a8.vec_out = a->vec_out;
+        }
         switch (a->p2) {
 #define SOS_SMALL(P2)                                                                              \
     case P2:                                                                                       \
         if (vec)                                                                                   \
-            hipLaunchKernelGGL((k_small_fold<T, OP, P2, true>), dim3(blocks), dim3(kThreads), 0, st, \
-                               (T *)out, *a, n);                                                   \
+            hipLaunchKernelGGL((k_small_fold<T, OP, P2, true, SmallFoldArgs8>), dim3(blocks),       \
+                               dim3(kThreads), 0, st, (T *)out, a8, n);                            \
         else                                                                                       \
-            hipLaunchKernelGGL((k_small_fold<T, OP, P2, false>), dim3(blocks), dim3(kThreads), 0, st, \
-                               (T *)out, *a, n);                                                   \
+            hipLaunchKernelGGL((k_small_fold<T, OP, P2, false, SmallFoldArgs8>), dim3(blocks),      \
+                               dim3(kThreads), 0, st, (T *)out, a8, n);                            \
         break;
             SOS_SMALL(1)
             SOS_SMALL(2)
@@ -210,8 +227,8 @@ struct SmallFoldFn {
             SOS_SMALL(8)
 #undef SOS_SMALL
             default:
-                hipLaunchKernelGGL((k_small_fold<T, OP, 0, false>), dim3(blocks), dim3(kThreads), 0, st,
-                                   (T *)out, *a, n);
+                hipLaunchKernelGGL((k_small_fold<T, OP, 0, false, SmallFoldArgs>), dim3(blocks),
+                                   dim3(kThreads), 0, st, (T *)out, *a, n);
         }
         return hip_ok(hipGetLastError());
     }

@@ -165,6 +165,24 @@ void wait_flags(int nb, uint32_t seq, const char *fn)
     }
 }
 
+// SOSX_SMALL_TRACE=N (diagnostics): host time per phase of small_path_reduce, averaged
+// over windows of N calls and printed to stderr (slot free, copy + post, peers' posts,
+// launch call, completion words, acks + copy out).
+struct SmallTrace {
+    int every = -1;
+    long calls = 0;
+    double t[6] = {0, 0, 0, 0, 0, 0};
+    bool on()
+    {
+        if (every < 0) {
+            const char *e = getenv("SOSX_SMALL_TRACE");
+            every = e ? atoi(e) : 0;
+        }
+        return every > 0;
+    }
+};
+SmallTrace g_strace;
+
 }  // namespace
 
 size_t small_shared_bytes(int npes)
@@ -253,9 +271,18 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     const size_t bytes = count * ts;
     const int P = t.size, me = t.my_idx, mw = s.my_pe;
     const int sl = (int)(g.seq++ % 2);
+    const bool tr = g_strace.on();
+    double tp = tr ? now_s() : 0;
+    auto phase = [&](int ph) {
+        if (!tr) return;
+        const double now = now_s();
+        g_strace.t[ph] += now - tp;
+        tp = now;
+    };
     // 1. my slot is free once every receiver of its previous post has read it
     for (const auto &u : g.slot_users[sl]) wait_ge(ctl(u.first)->consumed[mw].v, u.second, "a peer to read a slot");
     g.slot_users[sl].clear();
+    phase(0);
     memcpy(g.host + slot_off(mw, sl), source, bytes);
     // 2. publish it to the team, then take the peers' posts
     std::atomic_thread_fence(std::memory_order_release);
@@ -268,6 +295,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         mine->posted[r].v.store(k, std::memory_order_release);
         g.slot_users[sl].push_back({r, k});
     }
+    phase(1);
     const void *in[kMaxPE];
     int from[kMaxPE];
     for (int i = 0; i < P; ++i) {
@@ -283,6 +311,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         in[i] = g.dev + slot_off(q, qs);
         from[i] = q;
     }
+    phase(2);
     // the result goes straight into the host symmetric heap (device-mapped pinned
     // memory), else into the pinned result slot
     const bool direct = s.host_heap.contains(target, bytes);
@@ -314,13 +343,27 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         rc = sosx_small_fold(op, dt, out, leaves, extras, p2, count, g.flags, g.fseq, &nblocks, s.stream);
     }
     if (rc) raise_error("%s: small host-resident reduction failed (status %d)", fn, rc);
+    phase(3);
     // 4. completion from the workgroups' flags (no stream synchronisation); then the
     //    peers' slots are read: acknowledge; my result out
     wait_flags(nblocks, g.fseq, fn);
+    phase(4);
     for (int i = 0; i < P; ++i)
         if (from[i] >= 0) mine->consumed[from[i]].v.store(g.seen_from[from[i]], std::memory_order_release);
     if (!direct) memcpy(target, g.out, bytes);
     g.calls++;
+    if (tr) {
+        phase(5);
+        if (++g_strace.calls % g_strace.every == 0) {
+            const double k = 1e6 / (double)g_strace.every;
+            fprintf(stderr, "[%04d] small-path trace (calls %ld-%ld, us/call): slot %.2f copy+post %.2f "
+                    "peers %.2f launch %.2f done %.2f acks+out %.2f\n", s.my_pe,
+                    g_strace.calls - g_strace.every + 1, g_strace.calls, g_strace.t[0] * k,
+                    g_strace.t[1] * k, g_strace.t[2] * k, g_strace.t[3] * k, g_strace.t[4] * k,
+                    g_strace.t[5] * k);
+            for (double &v : g_strace.t) v = 0;
+        }
+    }
 }
 
 }  // namespace sosrt
