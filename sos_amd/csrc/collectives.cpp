@@ -698,8 +698,12 @@ int sos_api_broadcast(shmem_team_t team, void *dest, const void *source, size_t 
     check_root(PE_root, t->size, fn);
     if (bytes == 0) return 0;
     // the team forms copy source to dest on the root as well (collectives_c.c4:390-397)
-    execute(sosplan::bcast_alg(PE_root, true), dest, source, nelems, type_size, *t, SOSX_OP_SUM,
-            SOSX_DT_UCHAR, fn);
+    const int plan = sosplan::bcast_alg(PE_root, true);
+    if (t->size > 1 && small_path_takes(plan, dest, source, bytes, *t)) {
+        small_path_reduce(plan, dest, source, nelems, type_size, *t, SOSX_OP_SUM, SOSX_DT_UCHAR, fn);
+        return 0;
+    }
+    execute(plan, dest, source, nelems, type_size, *t, SOSX_OP_SUM, SOSX_DT_UCHAR, fn);
     return 0;
 }
 
@@ -724,8 +728,12 @@ static void bcast_active_set(void *target, const void *source, size_t nlong, siz
     t.my_idx = (s.my_pe - PE_start) / stride;
     t.valid = true;
     // the root's target is not written (collectives_c.c4:342-378)
-    execute(sosplan::bcast_alg(PE_root, false), target, source, nlong, ts, t, SOSX_OP_SUM,
-            SOSX_DT_UCHAR, fn);
+    const int plan = sosplan::bcast_alg(PE_root, false);
+    if (small_path_takes(plan, target, source, bytes, t)) {
+        small_path_reduce(plan, target, source, nlong, ts, t, SOSX_OP_SUM, SOSX_DT_UCHAR, fn);
+        return;
+    }
+    execute(plan, target, source, nlong, ts, t, SOSX_OP_SUM, SOSX_DT_UCHAR, fn);
 }
 
 void pshmem_broadcast32(void *target, const void *source, size_t nlong, int PE_root, int PE_start,

@@ -17,6 +17,7 @@
 //      - the ring (AUTO above it, sosx_small_ring): chunk c folded from PE c, every
 //        chunk evaluated by every PE (the allgather's result);
 //      - the team scans (sosx_small_linear): the in-order prefix of the team's sources;
+//      - the broadcasts (sosx_small_linear over one operand): the root's bytes;
 //   4. the result lands in `target` directly when it is in the (device-mapped) host
 //      symmetric heap, else in a pinned slot copied out; the host learns that the kernel
 //      finished from per-workgroup completion words in pinned memory, not from a
@@ -252,6 +253,8 @@ long small_path_calls() { return g.calls; }
 bool small_path_takes(int alg, const void *target, const void *source, size_t bytes, const Team &t)
 {
     if (!g.ready || bytes == 0 || bytes > g.slot || t.size < 2 || t.size > kMaxPE) return false;
+    if (sosplan::is_bcast(alg))  // every PE reads one operand, the root's
+        return bytes <= kTeamBytes && !is_device_ptr(source) && !is_device_ptr(target);
     if (bytes > kLatencyBytes && (size_t)t.size * bytes > kTeamBytes) return false;
     if (alg == SOSX_ALG_RING || sosplan::is_scan(alg)) {
         if ((size_t)t.size > kRingMaxPE) return false;
@@ -283,7 +286,10 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     for (const auto &u : g.slot_users[sl]) wait_ge(ctl(u.first)->consumed[mw].v, u.second, "a peer to read a slot");
     g.slot_users[sl].clear();
     phase(0);
-    memcpy(g.host + slot_off(mw, sl), source, bytes);
+    const bool bcast = sosplan::is_bcast(alg);
+    const int root = bcast ? (alg - sosplan::PLAN_BCAST) / 2 : -1;
+    // a broadcast reads only the root's operand; the others post an empty slot
+    if (!bcast || me == root) memcpy(g.host + slot_off(mw, sl), source, bytes);
     // 2. publish it to the team, then take the peers' posts
     std::atomic_thread_fence(std::memory_order_release);
     SmallCtl *mine = ctl(mw);
@@ -315,10 +321,20 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     // the result goes straight into the host symmetric heap (device-mapped pinned
     // memory), else into the pinned result slot
     const bool direct = s.host_heap.contains(target, bytes);
-    void *out = direct ? target : g.out;
+    void *out = direct ? target : g.out;  // null when this PE writes nothing
     if (++g.fseq == 0) g.fseq = 1;
     int rc = SOSX_OK, nblocks = 0;
-    if (sosplan::is_scan(alg)) {
+    if (bcast) {
+        // 3. one launch: the root's bytes into this PE's target -- every non-root, and the
+        //    root itself for the team forms (copy_root, src/collectives_c.c4:390-397); the
+        //    active-set forms leave the root's target untouched (:342-378)
+        const bool copy_root = ((alg - sosplan::PLAN_BCAST) & 1) != 0;
+        if (me != root || copy_root)
+            rc = sosx_small_linear(SOSX_OP_BOR, SOSX_DT_UCHAR, out, &in[root], 1, bytes, g.flags,
+                                   g.fseq, &nblocks, s.stream);
+        else
+            out = nullptr;  // nothing written: no copy out either
+    } else if (sosplan::is_scan(alg)) {
         // 3. one launch: the in-order prefix of the team's sources 0..me (inscan) or
         //    0..me-1 (exscan), the running value the left operand; exscan's PE 0 gets
         //    zeros, as SOS's memset (src/collectives.c:1111-1209)
@@ -350,7 +366,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     phase(4);
     for (int i = 0; i < P; ++i)
         if (from[i] >= 0) mine->consumed[from[i]].v.store(g.seen_from[from[i]], std::memory_order_release);
-    if (!direct) memcpy(target, g.out, bytes);
+    if (!direct && out) memcpy(target, g.out, bytes);
     g.calls++;
     if (tr) {
         phase(5);

@@ -156,10 +156,10 @@ def main():
                     src = gen(L.DTYPES["uchar"], seed, members[idx], n * es, 1)
                     rsrc = gen(L.DTYPES["uchar"], seed, members[root], n * es, 1)
                     init = torch.full_like(src, SENTINEL)
-                    for mode in ("heap", "heap_inplace", "device", "host"):
-                        if mode == "host" and n > 5003:
+                    for mode in ("heap", "heap_inplace", "device", "host", "hostheap"):
+                        if mode in ("host", "hostheap") and n > 5003:
                             continue
-                        got = Buffers(hsrc, hdst, n * es).run(
+                        got = Buffers(hsrc, hdst, n * es, hh).run(
                             mode, src, init, lambda d, s: fn(team, d, s, n, root))
                         # every PE ends with the root's data (the root copies too)
                         mm = L.count_mismatch(rsrc.data_ptr(), got.data_ptr(), n * es, 1)
@@ -173,10 +173,10 @@ def main():
                 src = gen(L.DTYPES["uchar"], seed, me, n * es, 1)
                 rsrc = gen(L.DTYPES["uchar"], seed, root, n * es, 1)
                 init = torch.full_like(src, SENTINEL)
-                for mode in ("heap", "device", "host"):
-                    if mode == "host" and n > 5003:
+                for mode in ("heap", "device", "host", "hostheap"):
+                    if mode in ("host", "hostheap") and n > 5003:
                         continue
-                    got = Buffers(hsrc, hdst, n * es).run(
+                    got = Buffers(hsrc, hdst, n * es, hh).run(
                         mode, src, init, lambda d, s: fn(d, s, n, root, 0, 0, P, psync))
                     exp = init[:n * es] if me == root else rsrc
                     mm = L.count_mismatch(exp.data_ptr(), got.data_ptr(), n * es, 1)

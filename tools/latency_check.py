@@ -112,6 +112,8 @@ def main():
     ap.add_argument("--legs", default="dev,host,cpu")
     ap.add_argument("--reps", type=int, default=int(os.environ.get("LAT_REPS", "200")))
     ap.add_argument("--ring", action="store_true", help="also the ring above the crossover (dev)")
+    ap.add_argument("--bcast", action="store_true",
+                    help="host-heap shmem_broadcastmem from PE 0 at the small sizes (replaces the legs)")
     ap.add_argument("--crossover", action="store_true",
                     help="host-heap AUTO vs SOS CPU AUTO from 16 KiB to 16 MiB (replaces the legs)")
     a = ap.parse_args()
@@ -123,6 +125,16 @@ def main():
     nmax = max(ring_sizes)
     scratch = S.lib().shmem_malloc(64)
     rows = []
+    if a.bcast:
+        legs = []
+        hs = S.lib().shmem_malloc(max(SMALL) * 4)
+        hd = S.lib().shmem_malloc(max(SMALL) * 4)
+        np.ctypeslib.as_array((ctypes.c_float * max(SMALL)).from_address(hs))[:] = 0.5 + me
+        for n in SMALL:
+            t = time_calls(lambda: S.shmem_broadcastmem(team, hd, hs, n * 4, 0), a.reps)
+            rows.append(("host", "bcast", n, max_over_pes(t, scratch)))
+        S.lib().shmem_free(hd)
+        S.lib().shmem_free(hs)
     if a.crossover:
         legs = []
         nmx = max(CROSS)
