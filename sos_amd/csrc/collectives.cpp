@@ -798,6 +798,9 @@ int shmemx_reduce_local(int op, int datatype, size_t count, const void *in, void
     if (rc || count == 0) return rc;
     if (!inout || !in) return SOSX_ERR_ARG;
     const bool dev_io = is_device_ptr(inout), dev_in = is_device_ptr(in);
+    // small operands, same residency: one launch, completion words (smallpath.cpp)
+    if (small_local_combine(op, datatype, inout, in, count, sosx_dtype_size(datatype), dev_io, dev_in))
+        return SOSX_OK;
     // both on the host (the SOS heap): H2D || combine || D2H pipeline, synchronous
     if (!dev_io && !dev_in) return sosx_combine_host(op, datatype, inout, in, count, 0);
     State &s = st();

@@ -791,6 +791,7 @@ void shmem_finalize(void)
     s.scratch_bytes = s.stage_bytes = 0;
     s.dbar = nullptr;
     sosx_combine_host_release();
+    small_local_release();
     if (s.stripes) (void)hipFree(s.stripes);
     s.stripes = nullptr;
     s.stripes_bytes = 0;

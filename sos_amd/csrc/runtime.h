@@ -193,6 +193,11 @@ bool small_path_takes(int alg, const void *target, const void *source, size_t by
 void small_path_reduce(int alg, void *target, const void *source, size_t count, size_t ts,
                        const Team &t, int op, int dt, const char *fn);
 long small_path_calls();
+// shmemx_reduce_local on operands of <= 64 KiB that are both in HBM or both in host memory:
+// one launch + completion words (smallpath.cpp); false = not taken, use the general path.
+bool small_local_combine(int op, int dt, void *inout, const void *in, size_t count, size_t ts,
+                         bool dev_io, bool dev_in);
+void small_local_release();
 void team_word_put(int which, int world_pe, uint64_t v);   // node shm (p2p.cpp)
 uint64_t team_word_get(int which, int world_pe);
 // p2p signalling mode (p2p.cpp): stream-ordered device signals on the registered shm

@@ -58,6 +58,7 @@ constexpr size_t kRingMaxPE = 8;                // sosx_small_ring's team sizes
 // The path takes P * bytes <= this.
 constexpr size_t kTeamBytes = (size_t)1 << 20;
 constexpr size_t kLatencyBytes = 16 * 1024;     // always taken when it fits a slot
+constexpr size_t kLocalCombineBytes = 64 * 1024;  // shmemx_reduce_local's small path
 
 // Slot bytes (the largest operand the path takes): SHMEMX_SMALL_HOST_BYTES (default
 // 1 MiB), capped so that 2 slots per PE stay within kSlotsCap, in 4 KiB units, at
@@ -141,12 +142,12 @@ void wait_ge(const std::atomic<uint64_t> &w, uint64_t v, const char *what)
 // ~12 us, a launch + flag poll ~6.6 us: profiles/r3_sync_probe.json).  Every 4096 polls
 // the stream is queried: an error, or a drained stream whose flags are still missing,
 // ends the job with a message, as does SHMEMX_P2P_TIMEOUT.
-void wait_flags(int nb, uint32_t seq, const char *fn)
+void wait_flags(const uint32_t *flags, int nb, uint32_t seq, const char *fn)
 {
     const double t0 = now_s();
     unsigned spins = 0;
     for (int b = 0; b < nb;) {
-        if (__atomic_load_n(g.flags + b, __ATOMIC_ACQUIRE) == seq) {
+        if (__atomic_load_n(flags + b, __ATOMIC_ACQUIRE) == seq) {
             ++b;
             continue;
         }
@@ -155,7 +156,7 @@ void wait_flags(int nb, uint32_t seq, const char *fn)
         const hipError_t e = hipStreamQuery(st().stream);
         if (e == hipSuccess) {  // drained: every flag must be visible by now
             for (int k = b; k < nb; ++k)
-                if (__atomic_load_n(g.flags + k, __ATOMIC_ACQUIRE) != seq)
+                if (__atomic_load_n(flags + k, __ATOMIC_ACQUIRE) != seq)
                     raise_error("%s: small host-resident reduction: workgroup %d of %d did not "
                                 "signal completion", fn, k, nb);
             return;
@@ -362,7 +363,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     phase(3);
     // 4. completion from the workgroups' flags (no stream synchronisation); then the
     //    peers' slots are read: acknowledge; my result out
-    wait_flags(nblocks, g.fseq, fn);
+    wait_flags(g.flags, nblocks, g.fseq, fn);
     phase(4);
     for (int i = 0; i < P; ++i)
         if (from[i] >= 0) mine->consumed[from[i]].v.store(g.seen_from[from[i]], std::memory_order_release);
@@ -380,6 +381,68 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
             for (double &v : g_strace.t) v = 0;
         }
     }
+}
+
+// ---------------------------------------------------------------------------------
+// Small local combines (shmemx_reduce_local, shmem_internal_reduce_local's slot in this
+// build): one launch of the LINEAR two-operand fold, out = inout OP in, with completion
+// words instead of a stream synchronisation.  Host operands in the host symmetric heap
+// (pinned, device-mapped) are read and written in place; other host memory goes through
+// two pinned staging buffers.  Per process, any number of PEs.
+// ---------------------------------------------------------------------------------
+namespace {
+struct LocalSmall {
+    char *stage = nullptr;     // 2 x kLocalBytes, pinned
+    uint32_t *flags = nullptr; // pinned, coherent
+    uint32_t seq = 0;
+    bool failed = false;
+};
+LocalSmall g_local_small;
+constexpr size_t kLocalFlagWords = kLocalCombineBytes / 256 + 8;
+}  // namespace
+
+bool small_local_combine(int op, int dt, void *inout, const void *in, size_t count, size_t ts,
+                         bool dev_io, bool dev_in)
+{
+    State &s = st();
+    const size_t bytes = count * ts;
+    if (bytes == 0 || bytes > kLocalCombineBytes || dev_io != dev_in) return false;
+    LocalSmall &L = g_local_small;
+    if (!L.flags && !L.failed) {
+        if (hipHostMalloc((void **)&L.flags, kLocalFlagWords * sizeof(uint32_t), hipHostMallocCoherent) != hipSuccess ||
+            hipHostMalloc((void **)&L.stage, 2 * kLocalCombineBytes, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            if (L.flags) (void)hipHostFree(L.flags);
+            L = LocalSmall();
+            L.failed = true;  // the general path serves every call
+        } else {
+            memset(L.flags, 0, kLocalFlagWords * sizeof(uint32_t));
+        }
+    }
+    if (L.failed) return false;
+    // operands: HBM and the host symmetric heap in place, other host memory staged
+    const bool stage_io = !dev_io && !s.host_heap.contains(inout, bytes);
+    const bool stage_in = !dev_in && !s.host_heap.contains(in, bytes);
+    void *io = stage_io ? L.stage : inout;
+    const void *ii = stage_in ? (const void *)(L.stage + kLocalCombineBytes) : in;
+    if (stage_io) memcpy(L.stage, inout, bytes);
+    if (stage_in) memcpy(L.stage + kLocalCombineBytes, in, bytes);
+    if (++L.seq == 0) L.seq = 1;
+    const void *ins[2] = {io, ii};
+    int nblocks = 0;
+    const int rc = sosx_small_linear(op, dt, io, ins, 2, count, L.flags, L.seq, &nblocks, s.stream);
+    if (rc) raise_error("shmemx_reduce_local: small combine failed (status %d)", rc);
+    wait_flags(L.flags, nblocks, L.seq, "shmemx_reduce_local");
+    if (stage_io) memcpy(inout, L.stage, bytes);
+    return true;
+}
+
+void small_local_release()
+{
+    LocalSmall &L = g_local_small;
+    if (L.flags) (void)hipHostFree(L.flags);
+    if (L.stage) (void)hipHostFree(L.stage);
+    L = LocalSmall();
 }
 
 }  // namespace sosrt

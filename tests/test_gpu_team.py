@@ -153,6 +153,67 @@ def test_reduce_local_mixed_residency(torch_cuda, shmem1, oracle, where):
     assert np.array_equal(in_h.view(np.uint32), b.view(np.uint32))  # `in` left untouched
 
 
+@pytest.mark.parametrize("dt,op", [(23, 5), (24, 6), (4, 3), (27, 6), (25, 5), (13, 2)])
+def test_reduce_local_small(torch_cuda, shmem1, oracle, dt, op):
+    """shmemx_reduce_local on operands of at most 64 KiB (one launch, completion words):
+    device / device, host heap / host heap (in place in pinned memory), pageable /
+    pageable and heap / pageable (staged), and an in-place call -- each bit for bit the
+    oracle's reduce_local, `in` untouched, the result there when the call returns."""
+    import ctypes
+    S, torch = shmem1, torch_cuda
+    es = S.lib().sosx_dtype_size(dt)
+    for n in (1, 7, 4097, 65536 // es):
+        dist = 1 if op == 6 else 0
+        if dt == 25:
+            a = np.random.default_rng(n).standard_normal(n).astype(np.longdouble)
+            b = np.random.default_rng(n + 1).standard_normal(n).astype(np.longdouble)
+        else:
+            a, b = oracle.fill(dt, dist, 5, 0, n), oracle.fill(dt, dist, 5, 1, n)
+        ref = a.copy()
+        oracle.reduce_local(op, dt, b, ref)
+        nb = n * es
+        ha, hb = S.lib().shmem_malloc(nb), S.lib().shmem_malloc(nb)
+        try:
+            for where in ("device", "heap", "pageable", "heap_pageable", "inplace_heap"):
+                if where == "device":
+                    io = torch.from_numpy(a.view(np.uint8).copy()).cuda()
+                    ii = torch.from_numpy(b.view(np.uint8).copy()).cuda()
+                    torch.cuda.synchronize()
+                    assert S.shmemx_reduce_local(op, dt, n, ii.data_ptr(), io.data_ptr()) == 0
+                    got = io.cpu().numpy().tobytes()
+                    want = ref.tobytes()
+                elif where in ("heap", "heap_pageable"):
+                    ctypes.memmove(ha, a.ctypes.data, nb)
+                    src = b.copy()
+                    if where == "heap":
+                        ctypes.memmove(hb, b.ctypes.data, nb)
+                        src_ptr = hb
+                    else:
+                        src_ptr = src.ctypes.data
+                    assert S.shmemx_reduce_local(op, dt, n, src_ptr, ha) == 0
+                    got = ctypes.string_at(ha, nb)
+                    want = ref.tobytes()
+                    assert src.tobytes() == b.tobytes()
+                elif where == "pageable":
+                    io, ii = a.copy(), b.copy()
+                    assert S.shmemx_reduce_local(op, dt, n, ii.ctypes.data, io.ctypes.data) == 0
+                    got, want = io.tobytes(), ref.tobytes()
+                    assert ii.tobytes() == b.tobytes()
+                else:  # inout == in, both the same host-heap buffer: out = a OP a
+                    ctypes.memmove(ha, a.ctypes.data, nb)
+                    self_ref = a.copy()
+                    oracle.reduce_local(op, dt, a.copy(), self_ref)
+                    assert S.shmemx_reduce_local(op, dt, n, ha, ha) == 0
+                    got, want = ctypes.string_at(ha, nb), self_ref.tobytes()
+                if dt == 25:  # x87 80-bit payload of each 16-B slot (6 padding bytes kept)
+                    got = b"".join(got[i:i + 10] for i in range(0, nb, 16))
+                    want = b"".join(want[i:i + 10] for i in range(0, nb, 16))
+                assert got == want, (dt, op, n, where)
+        finally:
+            S.lib().shmem_free(hb)
+            S.lib().shmem_free(ha)
+
+
 def _run(cmd, timeout=120, env=None):
     e = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
