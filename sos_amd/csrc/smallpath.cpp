@@ -154,7 +154,9 @@ void wait_flags(const uint32_t *flags, int nb, uint32_t seq, const char *fn)
         __builtin_ia32_pause();
         if ((++spins & 0xFFF) != 0) continue;
         const hipError_t e = hipStreamQuery(st().stream);
-        if (e == hipSuccess) {  // drained: every flag must be visible by now
+        if (e == hipSuccess) {  // drained: every flag must be visible by now (after the
+                                // runtime's own synchronisation at the latest)
+            hip_check(hipStreamSynchronize(st().stream), fn);
             for (int k = b; k < nb; ++k)
                 if (__atomic_load_n(flags + k, __ATOMIC_ACQUIRE) != seq)
                     raise_error("%s: small host-resident reduction: workgroup %d of %d did not "
