@@ -233,10 +233,17 @@ int sosx_set_rccl_allreduce(int mode);
  * device heap. */
 void sosx_p2p_flags(unsigned *host_register, unsigned *ipc_open);
 
-/* Team reductions that took the small host-resident path (operands in host memory,
- * recdbl_sw semantics, at most 64 KiB: node shared memory + one fold kernel reading
- * every PE's operand in place).  Introspection for tests and benchmarks. */
+/* Team collectives (reductions, scans, broadcasts) that took the small path through
+ * node shared memory (operands copied into shared slots, one kernel per PE reading every
+ * PE's slot in place), and how many of them had a device-resident
+ * operand (SHMEMX_SMALL_DEVICE).  Introspection for tests and benchmarks. */
 long sosx_small_path_calls(void);
+long sosx_small_path_device_calls(void);
+/* Limit for device-resident operands on that path: a call takes it when team size *
+ * operand bytes <= team_bytes (0: never; default SHMEMX_SMALL_DEVICE, 256 KiB).  Returns
+ * the previous limit.  Collective in effect: every PE of a team must hold the same limit
+ * when it calls, as the path choice is made on each PE. */
+size_t sosx_set_small_device_bytes(size_t team_bytes);
 
 /* Library / build identification. */
 const char *sosx_build_info(void);

@@ -88,6 +88,8 @@ _SIGS = {
                                      _c.c_size_t]),
     "sosx_build_info": (_c.c_char_p, []),
     "sosx_small_path_calls": (_c.c_long, []),
+    "sosx_small_path_device_calls": (_c.c_long, []),
+    "sosx_set_small_device_bytes": (_c.c_size_t, [_c.c_size_t]),
     "sosx_p2p_signal_mode": (_c.c_int, []),
     "sosx_set_p2p_signal_mode": (_c.c_int, [_c.c_int]),
     "sosx_set_rccl_allgather": (_c.c_int, [_c.c_int]),

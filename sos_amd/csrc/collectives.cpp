@@ -572,9 +572,9 @@ void op_to_all(void *target, const void *source, size_t count, size_t ts, const 
         alg = SOSX_ALG_RECHALVING;
     if (alg == SOSX_ALG_RECDBL_GATHER && sosplan::pow2_floor(t.size) > SOSX_MAX_FOLD)
         alg = SOSX_ALG_RECDBL;
-    // small host-resident operands (recdbl_sw below the crossover, the ring above it):
-    // through the node shared segment, one kernel reading every PE's operand in place
-    // (smallpath.cpp), no DMA copies
+    // small operands (recdbl_sw below the crossover, the ring above it; host-resident, or
+    // device-resident below SHMEMX_SMALL_DEVICE): through the node shared segment, one
+    // kernel reading every PE's operand in place (smallpath.cpp), no DMA copies
     if (!s.rccl_allreduce && small_path_takes(alg, target, source, bytes, t)) {
         small_path_reduce(alg, target, source, count, ts, t, op, dt, fn);
         return;
@@ -781,7 +781,7 @@ int sos_api_scan(shmem_team_t team, void *dest, const void *source, size_t nelem
         raise_error("%s: teams of more than %d PEs are not supported", fn, sosplan::PLAN_MAX_PE);
     const int plan = exclusive ? sosplan::PLAN_EXSCAN : sosplan::PLAN_INSCAN;
     if (t->size > 1 && small_path_takes(plan, dest, source, bytes, *t)) {
-        // small host-resident operands: one kernel per PE over node shared memory
+        // small operands: one kernel per PE over node shared memory (smallpath.cpp)
         small_path_reduce(plan, dest, source, nelems, type_size, *t, op, datatype, fn);
         return 0;
     }

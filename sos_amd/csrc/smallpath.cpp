@@ -1,4 +1,6 @@
-// smallpath.cpp -- team reductions of small HOST-resident operands without DMA copies.
+// smallpath.cpp -- team reductions of small operands through node shared memory, without
+// DMA copies: host-resident operands (SOS's own case) and, below a smaller limit, device
+// ones.
 //
 // SOS runs a reduction below SHMEM_COLL_SIZE_CROSSOVER as recdbl_sw on host memory
 // (src/shmem_collectives.h:192-195, src/collectives.c:850-984).  On the general path a
@@ -24,6 +26,15 @@
 //      stream synchronisation (about 5 us less per call).
 // The arithmetic stays on the GPU; the host only moves the caller's bytes into and out
 // of shared memory, as SOS's puts do.
+//
+// Device-resident operands (HBM) take the same path with two launches instead of one: a
+// copy kernel moves the source into the slot (step 1, completion words, then the post),
+// and the fold kernel writes the result into the device target directly.  That is two
+// launch + completion-word round trips (~6 us each) against the executors' exchange,
+// fold and call-completion wait (47 us at P = 2 on one GPU,
+// profiles/r3_rehearsal_n2_onegpu_small.json); above SHMEMX_SMALL_DEVICE bytes over the
+// team (P * bytes, default 256 KiB) the slot traffic over the host link costs more than
+// the exchange saves and the executors run the call.
 //
 // Slot reuse: each PE alternates between two data slots.  A post to receiver r carries
 // a per-pair index k (posted[q][r] = k) and the slot id (ring[q][r][k % 2]); receiver r
@@ -59,6 +70,7 @@ constexpr size_t kRingMaxPE = 8;                // sosx_small_ring's team sizes
 constexpr size_t kTeamBytes = (size_t)1 << 20;
 constexpr size_t kLatencyBytes = 16 * 1024;     // always taken when it fits a slot
 constexpr size_t kLocalCombineBytes = 64 * 1024;  // shmemx_reduce_local's small path
+constexpr size_t kDeviceTeamBytes = 256 * 1024;   // default P * bytes limit, device operands
 
 // Slot bytes (the largest operand the path takes): SHMEMX_SMALL_HOST_BYTES (default
 // 1 MiB), capped so that 2 slots per PE stay within kSlotsCap, in 4 KiB units, at
@@ -100,7 +112,9 @@ struct Small {
     void *out = nullptr;         // pinned result slot (hipHostMalloc, device-mapped)
     uint32_t *flags = nullptr;   // per-workgroup completion words (pinned, coherent)
     uint32_t fseq = 0;           // the value the current launch's workgroups store
+    size_t dev_team_bytes = 0;   // device operands: P * bytes limit (0: host operands only)
     long calls = 0;
+    long dev_calls = 0;          // of which with a device operand
 };
 Small g;
 
@@ -132,7 +146,7 @@ void wait_ge(const std::atomic<uint64_t> &w, uint64_t v, const char *what)
     while (w.load(std::memory_order_acquire) < v) {
         __builtin_ia32_pause();
         if ((++spins & 0xFFFF) == 0 && now_s() - t0 > limit_s())
-            raise_error("small host-resident reduction: timed out after %.0f s waiting for %s",
+            raise_error("small shared-memory path: timed out after %.0f s waiting for %s",
                         limit_s(), what);
     }
 }
@@ -159,13 +173,13 @@ void wait_flags(const uint32_t *flags, int nb, uint32_t seq, const char *fn)
             hip_check(hipStreamSynchronize(st().stream), fn);
             for (int k = b; k < nb; ++k)
                 if (__atomic_load_n(flags + k, __ATOMIC_ACQUIRE) != seq)
-                    raise_error("%s: small host-resident reduction: workgroup %d of %d did not "
+                    raise_error("%s: small shared-memory path: workgroup %d of %d did not "
                                 "signal completion", fn, k, nb);
             return;
         }
         if (e != hipErrorNotReady) hip_check(e, fn);
         if (now_s() - t0 > limit_s())
-            raise_error("%s: small host-resident reduction: timed out after %.0f s", fn, limit_s());
+            raise_error("%s: small shared-memory path: timed out after %.0f s", fn, limit_s());
     }
 }
 
@@ -237,9 +251,10 @@ void small_path_setup(void *region, size_t bytes)
     g.bytes = bytes;
     g.slot = slot;
     g.npes = s.n_pes;
+    g.dev_team_bytes = env_size("SHMEMX_SMALL_DEVICE", kDeviceTeamBytes);
     g.ready = ok != 0;
     if (!g.ready) small_path_teardown();
-    debug_msg("small host-resident path: %s", g.ready ? "on" : "off");
+    debug_msg("small shared-memory path: %s", g.ready ? "on" : "off");
 }
 
 void small_path_teardown()
@@ -251,21 +266,34 @@ void small_path_teardown()
 }
 
 long small_path_calls() { return g.calls; }
+long small_path_device_calls() { return g.dev_calls; }
+
+size_t small_path_set_device_bytes(size_t team_bytes)
+{
+    const size_t prev = g.dev_team_bytes;
+    g.dev_team_bytes = team_bytes;
+    return prev;
+}
 
 // Does a reduction of `bytes` with these operands over team t take the small path?
 bool small_path_takes(int alg, const void *target, const void *source, size_t bytes, const Team &t)
 {
     if (!g.ready || bytes == 0 || bytes > g.slot || t.size < 2 || t.size > kMaxPE) return false;
-    if (sosplan::is_bcast(alg))  // every PE reads one operand, the root's
-        return bytes <= kTeamBytes && !is_device_ptr(source) && !is_device_ptr(target);
-    if (bytes > kLatencyBytes && (size_t)t.size * bytes > kTeamBytes) return false;
+    const size_t team_bytes = (size_t)t.size * bytes;
+    if (is_device_ptr(source) || is_device_ptr(target)) {
+        if (team_bytes > g.dev_team_bytes) return false;
+    } else if (sosplan::is_bcast(alg)) {  // every PE reads one operand, the root's
+        if (bytes > kTeamBytes) return false;
+    } else if (bytes > kLatencyBytes && team_bytes > kTeamBytes) {
+        return false;
+    }
+    if (sosplan::is_bcast(alg)) return true;
     if (alg == SOSX_ALG_RING || sosplan::is_scan(alg)) {
         if ((size_t)t.size > kRingMaxPE) return false;
     } else if (alg != SOSX_ALG_RECDBL && alg != SOSX_ALG_RECDBL_GATHER) {
         return false;
     }
-    if (sosplan::pow2_floor(t.size) > SOSX_MAX_FOLD) return false;
-    return !is_device_ptr(source) && !is_device_ptr(target);
+    return sosplan::pow2_floor(t.size) <= SOSX_MAX_FOLD;
 }
 
 // recdbl_sw's (or, for alg RING, the ring's; for the scan plans, the scan's) value for
@@ -291,8 +319,21 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     phase(0);
     const bool bcast = sosplan::is_bcast(alg);
     const int root = bcast ? (alg - sosplan::PLAN_BCAST) / 2 : -1;
-    // a broadcast reads only the root's operand; the others post an empty slot
-    if (!bcast || me == root) memcpy(g.host + slot_off(mw, sl), source, bytes);
+    const bool dev_src = is_device_ptr(source), dev_dst = is_device_ptr(target);
+    // a broadcast reads only the root's operand; the others post an empty slot.  A device
+    // source reaches the slot through one copy launch, complete before the post.
+    if (!bcast || me == root) {
+        if (dev_src) {
+            if (++g.fseq == 0) g.fseq = 1;
+            int nb = 0;
+            const int rc = sosx_small_linear(SOSX_OP_BOR, SOSX_DT_UCHAR, g.dev + slot_off(mw, sl), &source,
+                                             1, bytes, g.flags, g.fseq, &nb, s.stream);
+            if (rc) raise_error("%s: small-path copy of a device operand failed (status %d)", fn, rc);
+            wait_flags(g.flags, nb, g.fseq, fn);
+        } else {
+            memcpy(g.host + slot_off(mw, sl), source, bytes);
+        }
+    }
     // 2. publish it to the team, then take the peers' posts
     std::atomic_thread_fence(std::memory_order_release);
     SmallCtl *mine = ctl(mw);
@@ -321,9 +362,9 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         from[i] = q;
     }
     phase(2);
-    // the result goes straight into the host symmetric heap (device-mapped pinned
-    // memory), else into the pinned result slot
-    const bool direct = s.host_heap.contains(target, bytes);
+    // the result goes straight into a device target or the host symmetric heap
+    // (device-mapped pinned memory), else into the pinned result slot
+    const bool direct = dev_dst || s.host_heap.contains(target, bytes);
     void *out = direct ? target : g.out;  // null when this PE writes nothing
     if (++g.fseq == 0) g.fseq = 1;
     int rc = SOSX_OK, nblocks = 0;
@@ -342,8 +383,14 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         //    0..me-1 (exscan), the running value the left operand; exscan's PE 0 gets
         //    zeros, as SOS's memset (src/collectives.c:1111-1209)
         const int np = alg == sosplan::PLAN_INSCAN ? me + 1 : me;
-        if (np == 0) memset(out, 0, bytes);
-        else rc = sosx_small_linear(op, dt, out, in, np, count, g.flags, g.fseq, &nblocks, s.stream);
+        if (np > 0) {
+            rc = sosx_small_linear(op, dt, out, in, np, count, g.flags, g.fseq, &nblocks, s.stream);
+        } else if (dev_dst) {
+            hip_check(hipMemsetAsync(out, 0, bytes, s.stream), fn);
+            hip_check(hipStreamSynchronize(s.stream), fn);
+        } else {
+            memset(out, 0, bytes);
+        }
     } else if (alg == SOSX_ALG_RING) {
         // 3. one launch: every ring chunk c folded LINEAR from PE c (the reduce-scatter's
         //    order), all chunks by every PE (the allgather's result)
@@ -361,7 +408,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         }
         rc = sosx_small_fold(op, dt, out, leaves, extras, p2, count, g.flags, g.fseq, &nblocks, s.stream);
     }
-    if (rc) raise_error("%s: small host-resident reduction failed (status %d)", fn, rc);
+    if (rc) raise_error("%s: small-path reduction failed (status %d)", fn, rc);
     phase(3);
     // 4. completion from the workgroups' flags (no stream synchronisation); then the
     //    peers' slots are read: acknowledge; my result out
@@ -371,6 +418,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         if (from[i] >= 0) mine->consumed[from[i]].v.store(g.seen_from[from[i]], std::memory_order_release);
     if (!direct && out) memcpy(target, g.out, bytes);
     g.calls++;
+    if (dev_src || dev_dst) g.dev_calls++;
     if (tr) {
         phase(5);
         if (++g_strace.calls % g_strace.every == 0) {
@@ -450,3 +498,8 @@ void small_local_release()
 }  // namespace sosrt
 
 extern "C" long sosx_small_path_calls(void) { return sosrt::small_path_calls(); }
+extern "C" long sosx_small_path_device_calls(void) { return sosrt::small_path_device_calls(); }
+extern "C" size_t sosx_set_small_device_bytes(size_t team_bytes)
+{
+    return sosrt::small_path_set_device_bytes(team_bytes);
+}

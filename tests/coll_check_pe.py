@@ -190,11 +190,13 @@ def main():
     if even.value:
         S.lib().shmem_team_destroy(even)
     sig = {1: "stream", 0: "host"}.get(L.lib().sosx_p2p_signal_mode(), "none")
+    small_dev = L.lib().sosx_small_path_device_calls()
     S.shmem_finalize()
     if bad:
         print(f"PE {me}/{P}: {len(bad)} of {checks} checks FAILED: {bad[:6]}", flush=True)
         return 1
-    print(f"PE {me}/{P}: {checks} checks OK (p2p signal {sig})", flush=True)
+    print(f"PE {me}/{P}: {checks} checks OK (p2p signal {sig}, small-path device calls {small_dev})",
+          flush=True)
     return 0
 
 

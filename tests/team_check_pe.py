@@ -193,11 +193,13 @@ def main():
     S.lib().shmem_free(hh_in)
     sig = {1: "stream", 0: "host"}.get(L.lib().sosx_p2p_signal_mode(), "none")
     small = L.lib().sosx_small_path_calls()
+    small_dev = L.lib().sosx_small_path_device_calls()
     S.shmem_finalize()
     if bad:
         print(f"PE {me}/{P}: {len(bad)} of {checks} checks FAILED: {bad[:6]}", flush=True)
         return 1
-    print(f"PE {me}/{P}: {checks} checks OK (p2p signal {sig}, small-path calls {small})", flush=True)
+    print(f"PE {me}/{P}: {checks} checks OK (p2p signal {sig}, small-path calls {small}, "
+          f"device {small_dev})", flush=True)
     return 0
 
 

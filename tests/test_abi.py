@@ -241,3 +241,13 @@ def test_small_ring_rejects_bad_args():
     assert L.sosx_small_ring(5, 23, None, ins, 2, 1, None, 1, ctypes.byref(nb), None) == -3      # no flags
     assert L.sosx_small_ring(0, 24, None, ins, 2, 1, 1, 1, ctypes.byref(nb), None) == -2         # and on double
     assert L.sosx_small_ring(5, 23, None, ins, 2, 0, 1, 1, ctypes.byref(nb), None) == 0 and nb.value == 0
+
+
+def test_small_device_bytes_setter():
+    """sosx_set_small_device_bytes returns the previous limit (host state only, CPU)."""
+    from sos_amd import _lib
+    L = _lib.lib()
+    prev = L.sosx_set_small_device_bytes(12345)
+    assert L.sosx_set_small_device_bytes(0) == 12345
+    assert L.sosx_set_small_device_bytes(prev) == 0
+    assert L.sosx_small_path_device_calls() == 0

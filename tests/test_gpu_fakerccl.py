@@ -67,8 +67,10 @@ def _used_fake(r, np_):
 
 @pytest.mark.parametrize("np_", [2, 3, 4])
 def test_team_check_rccl_executor(np_):
-    """Every schedule, 8 type/op pairs, heap / device / host buffers, in place, a split team."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900)
+    """Every schedule, 8 type/op pairs, heap / device / host buffers, in place, a split team
+    (small device operands on the executor too: SHMEMX_SMALL_DEVICE=0)."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
+               SHMEMX_SMALL_DEVICE="0")
     _ok(r, np_)
 
 
@@ -87,8 +89,9 @@ def test_team_check_rccl_native_allgather(np_):
 
 @pytest.mark.parametrize("np_", [3])
 def test_coll_check_rccl_executor(np_):
-    """Scans and broadcasts over the RCCL executor."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "coll_check_pe.py")], timeout=600)
+    """Scans and broadcasts over the RCCL executor (small device operands included)."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "coll_check_pe.py")], timeout=600,
+               SHMEMX_SMALL_DEVICE="0")
     _ok(r, np_)
 
 

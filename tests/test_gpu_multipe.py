@@ -63,22 +63,29 @@ def test_reduce_types_4_pes(examples):
     assert "reduce_types: OK (4 PEs)" in r.stdout
 
 
-@pytest.mark.parametrize("np_,signal", [(2, "stream"), (3, "stream"), (4, "stream"), (8, "stream"),
-                                         (3, "host"), (8, "host")])
-def test_team_check(np_, signal):
+@pytest.mark.parametrize("np_,signal,small_dev", [(2, "stream", True), (3, "stream", False),
+                                                   (4, "stream", True), (8, "stream", True),
+                                                   (3, "host", False), (8, "host", False)])
+def test_team_check(np_, signal, small_dev):
     """Every schedule across np_ PE processes, with the p2p transport's counters moved by
     stream-ordered device signals (the default) or by the host every round
-    (SHMEMX_P2P_SIGNAL=host)."""
+    (SHMEMX_P2P_SIGNAL=host); small device operands through node shared memory (the
+    default) or, with SHMEMX_SMALL_DEVICE=0, on the p2p executor like larger ones."""
+    env = {"SHMEMX_P2P_SIGNAL": signal}
+    if not small_dev:
+        env["SHMEMX_SMALL_DEVICE"] = "0"
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
-               extra_env={"SHMEMX_P2P_SIGNAL": signal})
+               extra_env=env)
     # PEs print concurrently, so lines may interleave: count the reports, not lines
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+), small-path calls (\d+)\)",
-                    r.stdout)
-    assert r.returncode == 0 and sorted(int(p) for p, _, _ in ok) == list(range(np_)), \
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+), small-path calls (\d+), "
+                    r"device (\d+)\)", r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _, _, _ in ok) == list(range(np_)), \
         r.stdout + r.stderr[-3000:]
-    assert {m for _, m, _ in ok} == {signal}, ok
-    # the host-resident recdbl_sw calls below 64 KiB took the shared-memory path
-    assert all(int(c) > 0 for _, _, c in ok), ok
+    assert {m for _, m, _, _ in ok} == {signal}, ok
+    # the host-resident recdbl_sw calls below 64 KiB took the shared-memory path, and the
+    # small device-resident ones did when it was on
+    assert all(int(c) > 0 for _, _, c, _ in ok), ok
+    assert all((int(d) > 0) == small_dev for _, _, _, d in ok), ok
 
 
 @pytest.mark.parametrize("np_", [2, 3])
@@ -87,7 +94,7 @@ def test_team_check_small_path_off(np_):
     (staged) path -- both paths give the oracle's bits."""
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
                extra_env={"SHMEMX_SMALL_HOST": "0"})
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal \w+, small-path calls (\d+)\)", r.stdout)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal \w+, small-path calls (\d+),", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
         r.stdout + r.stderr[-3000:]
     assert all(int(c) == 0 for _, c in ok), ok
@@ -99,23 +106,30 @@ def test_team_check_small_path_bytes():
     path did run."""
     r = oshrun(3, [sys.executable, os.path.join(ROOT, "tests", "team_check_pe.py")], timeout=900,
                extra_env={"SHMEMX_SMALL_HOST_BYTES": "4096"})
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal \w+, small-path calls (\d+)\)", r.stdout)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal \w+, small-path calls (\d+),", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == [0, 1, 2], \
         r.stdout + r.stderr[-3000:]
     assert all(int(c) > 0 for _, c in ok), ok
 
 
-@pytest.mark.parametrize("np_,signal", [(2, "host"), (3, "host"), (4, "host"), (8, "host"),
-                                         (3, "stream"), (8, "stream")])
-def test_coll_check(np_, signal):
+@pytest.mark.parametrize("np_,signal,small_dev", [(2, "host", True), (3, "host", True),
+                                                   (4, "host", False), (8, "host", True),
+                                                   (3, "stream", True), (8, "stream", False)])
+def test_coll_check(np_, signal, small_dev):
     """Scans and broadcasts through the public API (tests/coll_check_pe.py), p2p counters
-    moved by the host or by stream-ordered device signals."""
+    moved by the host or by stream-ordered device signals; small device operands through
+    node shared memory or (SHMEMX_SMALL_DEVICE=0) on the executor."""
+    env = {"SHMEMX_P2P_SIGNAL": signal}
+    if not small_dev:
+        env["SHMEMX_SMALL_DEVICE"] = "0"
     r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "coll_check_pe.py")], timeout=900,
-               extra_env={"SHMEMX_P2P_SIGNAL": signal})
-    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+)[,)]", r.stdout)
-    assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
+               extra_env=env)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(p2p signal (\w+), small-path device calls (\d+)\)",
+                    r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _, _ in ok) == list(range(np_)), \
         r.stdout + r.stderr[-3000:]
-    assert {m for _, m in ok} == {signal}, ok
+    assert {m for _, m, _ in ok} == {signal}, ok
+    assert all((int(d) > 0) == small_dev for _, _, d in ok), ok
 
 
 @pytest.mark.parametrize("signal", ["stream", "host"])
@@ -131,15 +145,16 @@ def test_p2p_wait_is_bounded(signal):
     assert time.monotonic() - t0 < 55, "the job outlived the late PE's sleep"
 
 
-def test_small_path_wait_is_bounded():
-    """The same late PE with host-heap operands: the call takes the small host-resident
-    path (node shared memory), whose waits for a peer's operand are bounded by
-    SHMEMX_P2P_TIMEOUT too."""
+@pytest.mark.parametrize("mode", ["host", "devsmall"])
+def test_small_path_wait_is_bounded(mode):
+    """The same late PE with 64-float operands in the host heap or the device heap: the
+    call takes the small path through node shared memory, whose waits for a peer's operand
+    are bounded by SHMEMX_P2P_TIMEOUT too."""
     t0 = time.monotonic()
-    r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "p2p_timeout_pe.py"), "host"],
+    r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "p2p_timeout_pe.py"), mode],
                timeout=150, extra_env={"SHMEMX_P2P_TIMEOUT": "3"})
     assert r.returncode != 0, r.stdout
-    assert "small host-resident reduction: timed out" in r.stderr, r.stderr[-2000:]
+    assert "small shared-memory path: timed out" in r.stderr, r.stderr[-2000:]
     assert "reduction returned" not in r.stdout
     assert time.monotonic() - t0 < 55, "the job outlived the late PE's sleep"
 
@@ -215,7 +230,11 @@ def test_bench_team_leg(np_):
     assert [r["nreduce"] for r in small] == [1, 1024, 16384, 65536]
     for row in small:
         assert row["host_us"] > 0 and row["device_us"] > 0 and row["cpu_us"] > 0, row
+        assert row["device_executor_us"] > 0, row
         assert row["host_bitwise_mismatches_vs_cpu_all_ranks"] == 0, row
+        assert row["device_bitwise_mismatches_vs_cpu_all_ranks"] == 0, row
+    # the device-heap calls with team size * bytes <= 256 KiB took the shared-memory path
+    assert res["small_messages"]["small_path_device_calls_rank0_side"] > 0, res["small_messages"]
     # SOS's ring on np_ host processes beside the line, equal to the GPU ring byte for byte
     cpu = res["cpu_ring_baseline"]
     assert cpu["cores"] == np_ and cpu["value"] > 0 and cpu["kind"] == "port", cpu

@@ -13,6 +13,10 @@ collective).  Legs:
 Schedules: recdbl (recdbl_sw butterfly), recdbl_gather (one all-gather round + every
 PE's own tree: AUTO below the crossover), ring (AUTO above it).
 
+--crossover-dev: device-heap operands through the library under AUTO at 4 B .. 1 MiB (run
+once with SHMEMX_SMALL_DEVICE=0, the executors, and once with it large, the shared-memory
+small path wherever a slot fits): where the small path's limit for device operands lies.
+
 --crossover: host-heap operands through the library under AUTO, and SOS's CPU under its
 own AUTO rule (recdbl_sw below SHMEM_COLL_SIZE_CROSSOVER = 16 KiB, ring above,
 src/shmem_collectives.h:180-199), from 16 KiB to 16 MiB: where the GPU path starts to
@@ -35,6 +39,7 @@ from sos_amd import shmem as S  # noqa: E402
 
 SMALL = [1, 64, 1024, 4095]      # fp32: up to 16380 B, below the 16 KiB crossover
 CROSS = [4095, 16384, 65536, 262144, 1 << 20, 1 << 22]   # fp32: 16 KiB .. 16 MiB
+CROSS_DEV = [1, 1024, 4095, 16384, 65536, 262144]       # fp32: 4 B .. 1 MiB
 
 
 def max_over_pes(v, scratch):
@@ -114,6 +119,8 @@ def main():
     ap.add_argument("--ring", action="store_true", help="also the ring above the crossover (dev)")
     ap.add_argument("--bcast", action="store_true",
                     help="host-heap shmem_broadcastmem from PE 0 at the small sizes (replaces the legs)")
+    ap.add_argument("--crossover-dev", action="store_true",
+                    help="device-heap AUTO from 4 B to 1 MiB (replaces the legs)")
     ap.add_argument("--crossover", action="store_true",
                     help="host-heap AUTO vs SOS CPU AUTO from 16 KiB to 16 MiB (replaces the legs)")
     a = ap.parse_args()
@@ -135,6 +142,24 @@ def main():
             rows.append(("host", "bcast", n, max_over_pes(t, scratch)))
         S.lib().shmem_free(hd)
         S.lib().shmem_free(hs)
+    if a.crossover_dev:
+        legs = []
+        nmx = max(CROSS_DEV)
+        src = S.shmemx_malloc_device(nmx * 4)
+        dst = S.shmemx_malloc_device(nmx * 4)
+        L.fill(23, 0, 7, me, src, nmx)
+        S.shmemx_set_reduce_algorithm(L.ALGS["auto"])
+        before = L.lib().sosx_small_path_device_calls()
+        for n in CROSS_DEV:
+            r = max(10, min(a.reps, int(a.reps * 4096 / max(n, 4096))))
+            t = time_calls(lambda: S.shmem_float_sum_reduce(team, dst, src, n), r)
+            rows.append(("dev", "auto", n, max_over_pes(t, scratch)))
+        small_dev = L.lib().sosx_small_path_device_calls() - before
+        S.shmemx_free_device(dst)
+        S.shmemx_free_device(src)
+        if me == 0:
+            print(f"# SHMEMX_SMALL_DEVICE={os.environ.get('SHMEMX_SMALL_DEVICE', 'default')}: "
+                  f"{small_dev} device calls on PE 0 took the small path", flush=True)
     if a.crossover:
         legs = []
         nmx = max(CROSS)

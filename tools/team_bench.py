@@ -530,12 +530,16 @@ def small_messages(args, torch, dist, L, S, team, rank, world, stream):
     processes:
       host   : operands in the host symmetric heap (shmem_malloc), SOS's own case -- the
                small host-resident path (one kernel per PE over node shared memory);
-      device : operands in the device symmetric heap (shmemx_malloc_device), on the
-               library's default transport;
+      device : operands in the device symmetric heap (shmemx_malloc_device), as the
+               library runs them: through node shared memory while team size * bytes
+               <= SHMEMX_SMALL_DEVICE (256 KiB), else on the default transport;
+      device_executor : the same calls with that limit at 0 (every call on the
+               transport's executor);
       cpu    : SOS AUTO on the CPU -- recdbl_sw below 16 KiB, the ring above
                (oracle_pe_recdbl / oracle_pe_ring, src/collectives.c:850-984, :647-764),
                one pinned physical core per PE, memcpy puts over /dev/shm.
-    At every size the host-heap result is compared byte for byte with the CPU result.
+    At every size the host-heap and device-heap results are compared byte for byte with
+    the CPU result.
     Test infrastructure in the timed-baseline role only."""
     import numpy as np
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -568,6 +572,7 @@ def small_messages(args, torch, dist, L, S, team, rank, world, stream):
         return el.item() / reps
 
     small_before = S.lib().sosx_small_path_calls()
+    small_dev_before = S.lib().sosx_small_path_device_calls()
     rows = []
     for n in sizes:
         reps = 200 if n <= 16384 else 50
@@ -577,6 +582,13 @@ def small_messages(args, torch, dist, L, S, team, rank, world, stream):
                      "schedule": "recdbl_sw" if n * es < 16384 else "ring",
                      "host_us": round(th * 1e6, 2), "device_us": round(td * 1e6, 2)})
     small_calls = S.lib().sosx_small_path_calls() - small_before
+    small_dev_calls = S.lib().sosx_small_path_device_calls() - small_dev_before
+    cap = S.lib().sosx_set_small_device_bytes(0)     # every rank: the choice is per PE
+    for row in rows:
+        n = row["nreduce"]
+        tx = timed(lambda: S.shmem_float_sum_reduce(team, ddst, dsrc, n), 200 if n <= 16384 else 50)
+        row["device_executor_us"] = round(tx * 1e6, 2)
+    S.lib().sosx_set_small_device_bytes(cap)
 
     # SOS's CPU path on the same ranks, pinned one physical core each
     allowed = sorted(os.sched_getaffinity(0))
@@ -619,10 +631,18 @@ def small_messages(args, torch, dist, L, S, team, rank, world, stream):
             S.shmem_float_sum_reduce(team, hdst, hsrc, n)
             got = np.ctypeslib.as_array((ctypes_u8 * (n * es)).from_address(hdst)).copy()
             exp = ring.target().view(np.uint8)[:n * es].copy()
-            mm = torch.tensor([int(np.count_nonzero(got.view(np.uint32) != exp.view(np.uint32)))],
+            # ... and the device-heap result (the path the device row timed)
+            S.shmem_float_sum_reduce(team, ddst, dsrc, n)
+            gd = torch.empty(n * es, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            L.check(S.lib().sosx_memcpy(gd.data_ptr(), ddst, n * es, None), "sosx_memcpy")
+            gd = gd.cpu().numpy()
+            mm = torch.tensor([int(np.count_nonzero(got.view(np.uint32) != exp.view(np.uint32))),
+                               int(np.count_nonzero(gd.view(np.uint32) != exp.view(np.uint32)))],
                               dtype=torch.int64)
             dist.all_reduce(mm, op=dist.ReduceOp.SUM)
-            row["host_bitwise_mismatches_vs_cpu_all_ranks"] = int(mm.item())
+            row["host_bitwise_mismatches_vs_cpu_all_ranks"] = int(mm[0].item())
+            row["device_bitwise_mismatches_vs_cpu_all_ranks"] = int(mm[1].item())
             ring.barrier()
     finally:
         if ring is not None:
@@ -634,12 +654,17 @@ def small_messages(args, torch, dist, L, S, team, rank, world, stream):
     S.lib().shmem_free(hsrc)
     if rank == 0:
         for r in rows:
-            log(f"[small] n={r['nreduce']} host {r['host_us']} us, device {r['device_us']} us, "
-                f"SOS CPU {r['cpu_us']} us, mismatches {r['host_bitwise_mismatches_vs_cpu_all_ranks']}")
+            log(f"[small] n={r['nreduce']} host {r['host_us']} us, device {r['device_us']} us "
+                f"(executor {r['device_executor_us']} us), SOS CPU {r['cpu_us']} us, mismatches "
+                f"{r['host_bitwise_mismatches_vs_cpu_all_ranks']}/{r['device_bitwise_mismatches_vs_cpu_all_ranks']}")
     return {"op": "float sum", "algorithm": "auto", "rows": rows,
             "small_path_calls_rank0_side": int(small_calls),
-            "note": "us per call, max over ranks; host = host symmetric heap (small host-resident "
-                    "path), device = device symmetric heap (default transport), cpu = SOS AUTO "
+            "small_path_device_calls_rank0_side": int(small_dev_calls),
+            "small_device_team_bytes": int(cap),
+            "note": "us per call, max over ranks; host = host symmetric heap (small path through "
+                    "node shared memory), device = device symmetric heap (that path while team size "
+                    "* bytes <= small_device_team_bytes, else the default transport), "
+                    "device_executor = device heap on the default transport, cpu = SOS AUTO "
                     "on the CPU (recdbl_sw < 16 KiB, ring above), one pinned core per PE"}
 
 
