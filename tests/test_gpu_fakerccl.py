@@ -113,8 +113,10 @@ def test_team_management_small_path(np_=4):
 
 
 def test_api_sweep_rccl(np_=2):
-    """All 154 typed reductions and 44 to_all entry points through the public API."""
-    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "api_sweep_pe.py")], timeout=600)
+    """All 154 typed reductions and 44 to_all entry points through the public API (small
+    device operands on the executor too: SHMEMX_SMALL_DEVICE=0)."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "api_sweep_pe.py")], timeout=600,
+               SHMEMX_SMALL_DEVICE="0")
     _ok(r, np_)
 
 
