@@ -240,7 +240,7 @@ void sosx_p2p_flags(unsigned *host_register, unsigned *ipc_open);
 long sosx_small_path_calls(void);
 long sosx_small_path_device_calls(void);
 /* Limit for device-resident operands on that path: a call takes it when team size *
- * operand bytes <= team_bytes (0: never; default SHMEMX_SMALL_DEVICE, 256 KiB).  Returns
+ * operand bytes <= team_bytes (0: never; default SHMEMX_SMALL_DEVICE, 128 KiB).  Returns
  * the previous limit.  Collective in effect: every PE of a team must hold the same limit
  * when it calls, as the path choice is made on each PE. */
 size_t sosx_set_small_device_bytes(size_t team_bytes);

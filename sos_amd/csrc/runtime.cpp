@@ -257,7 +257,7 @@ static const EnvDef kEnv[] = {
      "Host-resident team reductions of small operands through node shared memory"},
     {"SHMEMX_SMALL_HOST_BYTES", "size", "1048576", "device",
      "Largest operand of that path (its slots: at most 32 MiB over all PEs)"},
-    {"SHMEMX_SMALL_DEVICE", "size", "262144", "device",
+    {"SHMEMX_SMALL_DEVICE", "size", "131072", "device",
      "Device-resident operands take that path when team size * bytes <= this (0: never)"},
 };
 

@@ -30,11 +30,13 @@
 // Device-resident operands (HBM) take the same path with two launches instead of one: a
 // copy kernel moves the source into the slot (step 1, completion words, then the post),
 // and the fold kernel writes the result into the device target directly.  That is two
-// launch + completion-word round trips (~6 us each) against the executors' exchange,
-// fold and call-completion wait (47 us at P = 2 on one GPU,
-// profiles/r3_rehearsal_n2_onegpu_small.json); above SHMEMX_SMALL_DEVICE bytes over the
-// team (P * bytes, default 256 KiB) the slot traffic over the host link costs more than
-// the exchange saves and the executors run the call.
+// launch + completion-word round trips against the executors' exchange, fold and
+// call-completion wait.  Measured with P PEs on one GPU, fp32 sum under AUTO
+// (profiles/r3_small_latency.txt, run dx): 20 / 23 / 72 us per 4-byte call at P = 2 / 4 /
+// 8 against 40 / 46 / 173 on the p2p executor; the executor wins again from P * bytes =
+// 256 KiB at P = 4 (64 vs 56 us) and 512 KiB at P = 2 (72 vs 49), where the slot traffic
+// over the host link costs more than the exchange saves.  The path takes device operands
+// while P * bytes <= SHMEMX_SMALL_DEVICE (default 128 KiB).
 //
 // Slot reuse: each PE alternates between two data slots.  A post to receiver r carries
 // a per-pair index k (posted[q][r] = k) and the slot id (ring[q][r][k % 2]); receiver r
@@ -70,7 +72,7 @@ constexpr size_t kRingMaxPE = 8;                // sosx_small_ring's team sizes
 constexpr size_t kTeamBytes = (size_t)1 << 20;
 constexpr size_t kLatencyBytes = 16 * 1024;     // always taken when it fits a slot
 constexpr size_t kLocalCombineBytes = 64 * 1024;  // shmemx_reduce_local's small path
-constexpr size_t kDeviceTeamBytes = 256 * 1024;   // default P * bytes limit, device operands
+constexpr size_t kDeviceTeamBytes = 128 * 1024;   // default P * bytes limit, device operands
 
 // Slot bytes (the largest operand the path takes): SHMEMX_SMALL_HOST_BYTES (default
 // 1 MiB), capped so that 2 slots per PE stay within kSlotsCap, in 4 KiB units, at

@@ -233,7 +233,7 @@ def test_bench_team_leg(np_):
         assert row["device_executor_us"] > 0, row
         assert row["host_bitwise_mismatches_vs_cpu_all_ranks"] == 0, row
         assert row["device_bitwise_mismatches_vs_cpu_all_ranks"] == 0, row
-    # the device-heap calls with team size * bytes <= 256 KiB took the shared-memory path
+    # the device-heap calls with team size * bytes <= 128 KiB took the shared-memory path
     assert res["small_messages"]["small_path_device_calls_rank0_side"] > 0, res["small_messages"]
     # SOS's ring on np_ host processes beside the line, equal to the GPU ring byte for byte
     cpu = res["cpu_ring_baseline"]

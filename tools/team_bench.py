@@ -532,7 +532,7 @@ def small_messages(args, torch, dist, L, S, team, rank, world, stream):
                small host-resident path (one kernel per PE over node shared memory);
       device : operands in the device symmetric heap (shmemx_malloc_device), as the
                library runs them: through node shared memory while team size * bytes
-               <= SHMEMX_SMALL_DEVICE (256 KiB), else on the default transport;
+               <= SHMEMX_SMALL_DEVICE (128 KiB), else on the default transport;
       device_executor : the same calls with that limit at 0 (every call on the
                transport's executor);
       cpu    : SOS AUTO on the CPU -- recdbl_sw below 16 KiB, the ring above
