@@ -237,6 +237,13 @@ void sosx_p2p_flags(unsigned *host_register, unsigned *ipc_open);
  * node shared memory (operands copied into shared slots, one kernel per PE reading every
  * PE's slot in place), and how many of them had a device-resident
  * operand (SHMEMX_SMALL_DEVICE).  Introspection for tests and benchmarks. */
+/* The small path's staging of a device-resident operand: one workgroup copies `bytes`
+ * from src (device) to dst (a node-shared slot, device view), fences at system scope and
+ * then stores vals[k] into *words[k], k < nwords (release, system scope: the slot's
+ * posts).  bytes <= SOSX_SMALL_FOLD_MAX, 1 <= nwords <= SOSX_MAX_FOLD. */
+int sosx_small_stage(void *dst, const void *src, size_t bytes, uint64_t *const *words,
+                     const uint64_t *vals, int nwords, void *stream);
+
 long sosx_small_path_calls(void);
 long sosx_small_path_device_calls(void);
 /* Limit for device-resident operands on that path: a call takes it when team size *

@@ -189,6 +189,49 @@ __global__ __launch_bounds__(kThreads) void k_small_ring(T *out, SmallRingArgs a
     signal_done(a.flags, a.seq);
 }
 
+// Staging of a device-resident operand (smallpath.cpp): one workgroup copies `bytes` from
+// HBM into the PE's slot of node shared memory (host memory, device view), fences at
+// system scope, and then publishes the slot itself: word k <- val[k] (release, system
+// scope), the posts the host makes for host operands.  With one workgroup the posts follow
+// every lane's stores without a grid-wide barrier; a slot is at most a few tens of KiB.
+// N = 8: 136 B of arguments for teams of up to 9 PEs (the launch call copies them).
+template <int N> struct SmallStageArgsT {
+    const void *src;
+    void *dst;
+    uint64_t bytes;
+    uint64_t *word[N];
+    uint64_t val[N];
+    int nwords;
+    int vec;                           // src and dst 16-B aligned
+};
+constexpr int kStageThreads = 1024;
+
+template <class A>
+__global__ __launch_bounds__(kStageThreads) void k_small_stage(A a)
+{
+    const uint8_t *s = (const uint8_t *)a.src;
+    uint8_t *d = (uint8_t *)a.dst;
+    uint64_t done = 0;
+    if (a.vec) {  // four 16-B loads in flight per lane (64 KiB per pass)
+        const uint64_t nv = a.bytes / 16;
+        for (uint64_t i = threadIdx.x; i < nv; i += 4 * kStageThreads) {
+            u32x4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + u * kStageThreads < nv) x[u] = reinterpret_cast<const u32x4 *>(s)[i + u * kStageThreads];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + u * kStageThreads < nv) reinterpret_cast<u32x4 *>(d)[i + u * kStageThreads] = x[u];
+        }
+        done = nv * 16;
+    }
+    for (uint64_t i = done + threadIdx.x; i < a.bytes; i += kStageThreads) d[i] = s[i];
+    __threadfence_system();
+    __syncthreads();
+    if ((int)threadIdx.x < a.nwords)
+        __hip_atomic_store(a.word[threadIdx.x], a.val[threadIdx.x], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace sos
 
 using namespace sos;
@@ -391,6 +434,51 @@ int sosx_small_linear(int op, int dtype, void *out, const void *const *ins, int 
     *nblocks = (int)tiles;
     return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles,
                                  as_stream(stream));
+}
+
+// Copy `bytes` from src (device) to dst (a node-shared slot, device view) in one
+// workgroup, then store vals[k] into *words[k] for k < nwords (release, system scope):
+// the small path's staging + post of a device operand.  bytes <= SOSX_SMALL_FOLD_MAX,
+// 1 <= nwords <= SOSX_MAX_FOLD.
+int sosx_small_stage(void *dst, const void *src, size_t bytes, uint64_t *const *words,
+                     const uint64_t *vals, int nwords, void *stream)
+{
+    if (!dst || !src || bytes > SOSX_SMALL_FOLD_MAX || nwords < 1 || nwords > SOSX_MAX_FOLD || !words ||
+        !vals)
+        return SOSX_ERR_ARG;
+    for (int k = 0; k < nwords; ++k)
+        if (!words[k]) return SOSX_ERR_ARG;
+    const hipStream_t st = as_stream(stream);
+    const int vec = aligned16(src) && aligned16(dst);
+    if (nwords <= 8) {
+        SmallStageArgsT<8> a;
+        memset(&a, 0, sizeof(a));
+        a.src = src;
+        a.dst = dst;
+        a.bytes = bytes;
+        for (int k = 0; k < nwords; ++k) {
+            a.word[k] = words[k];
+            a.val[k] = vals[k];
+        }
+        a.nwords = nwords;
+        a.vec = vec;
+        hipLaunchKernelGGL((k_small_stage<SmallStageArgsT<8>>), dim3(1), dim3(kStageThreads), 0, st, a);
+    } else {
+        SmallStageArgsT<SOSX_MAX_FOLD> a;
+        memset(&a, 0, sizeof(a));
+        a.src = src;
+        a.dst = dst;
+        a.bytes = bytes;
+        for (int k = 0; k < nwords; ++k) {
+            a.word[k] = words[k];
+            a.val[k] = vals[k];
+        }
+        a.nwords = nwords;
+        a.vec = vec;
+        hipLaunchKernelGGL((k_small_stage<SmallStageArgsT<SOSX_MAX_FOLD>>), dim3(1), dim3(kStageThreads), 0,
+                           st, a);
+    }
+    return hip_ok(hipGetLastError());
 }
 
 }  // extern "C"

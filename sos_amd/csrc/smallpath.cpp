@@ -28,10 +28,10 @@
 // of shared memory, as SOS's puts do.
 //
 // Device-resident operands (HBM) take the same path with two launches instead of one: a
-// copy kernel moves the source into the slot (step 1, completion words, then the post),
-// and the fold kernel writes the result into the device target directly.  That is two
-// launch + completion-word round trips against the executors' exchange, fold and
-// call-completion wait.  Measured with P PEs on one GPU, fp32 sum under AUTO
+// one-workgroup copy kernel moves the source into the slot and then stores the posts
+// itself (steps 1-2 on the device), and the fold kernel, queued behind it, writes the
+// result into the device target directly: one more launch, against the executors'
+// exchange, fold and call-completion wait.  Measured with P PEs on one GPU, fp32 sum under AUTO
 // (profiles/r3_small_latency.txt, run dx): 20 / 23 / 72 us per 4-byte call at P = 2 / 4 /
 // 8 against 40 / 46 / 173 on the p2p executor; the executor wins again from P * bytes =
 // 256 KiB at P = 4 (64 vs 56 us) and 512 KiB at P = 2 (72 vs 49), where the slot traffic
@@ -323,29 +323,34 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     const int root = bcast ? (alg - sosplan::PLAN_BCAST) / 2 : -1;
     const bool dev_src = is_device_ptr(source), dev_dst = is_device_ptr(target);
     // a broadcast reads only the root's operand; the others post an empty slot.  A device
-    // source reaches the slot through one copy launch, complete before the post.
-    if (!bcast || me == root) {
-        if (dev_src) {
-            if (++g.fseq == 0) g.fseq = 1;
-            int nb = 0;
-            const int rc = sosx_small_linear(SOSX_OP_BOR, SOSX_DT_UCHAR, g.dev + slot_off(mw, sl), &source,
-                                             1, bytes, g.flags, g.fseq, &nb, s.stream);
-            if (rc) raise_error("%s: small-path copy of a device operand failed (status %d)", fn, rc);
-            wait_flags(g.flags, nb, g.fseq, fn);
-        } else {
-            memcpy(g.host + slot_off(mw, sl), source, bytes);
-        }
-    }
+    // source reaches the slot through a one-workgroup copy launch that then makes the
+    // posts itself (sosx_small_stage), so the host goes straight on to the peers' posts
+    // and the fold launch queues behind the copy on the stream.
+    const bool staged = dev_src && (!bcast || me == root);
+    if ((!bcast || me == root) && !staged) memcpy(g.host + slot_off(mw, sl), source, bytes);
     // 2. publish it to the team, then take the peers' posts
     std::atomic_thread_fence(std::memory_order_release);
     SmallCtl *mine = ctl(mw);
+    uint64_t *words[kMaxPE];
+    uint64_t vals[kMaxPE];
+    int nw = 0;
     for (int i = 0; i < P; ++i) {
         if (i == me) continue;
         const int r = t.world_rank(i);
         const uint64_t k = ++g.posted_to[r];
         mine->ring[r][k % 2] = (uint32_t)sl;
-        mine->posted[r].v.store(k, std::memory_order_release);
+        if (staged) {  // the copy kernel's post: the device view of the same word
+            words[nw] = (uint64_t *)(g.dev + ((char *)&mine->posted[r].v - g.host));
+            vals[nw++] = k;
+        } else {
+            mine->posted[r].v.store(k, std::memory_order_release);
+        }
         g.slot_users[sl].push_back({r, k});
+    }
+    if (staged) {
+        std::atomic_thread_fence(std::memory_order_seq_cst);  // the slot ids before the launch
+        const int rc = sosx_small_stage(g.dev + slot_off(mw, sl), source, bytes, words, vals, nw, s.stream);
+        if (rc) raise_error("%s: small-path copy of a device operand failed (status %d)", fn, rc);
     }
     phase(1);
     const void *in[kMaxPE];

@@ -251,3 +251,21 @@ def test_small_device_bytes_setter():
     assert L.sosx_set_small_device_bytes(0) == 12345
     assert L.sosx_set_small_device_bytes(prev) == 0
     assert L.sosx_small_path_device_calls() == 0
+
+
+def test_small_stage_rejects_bad_args():
+    """sosx_small_stage validates before any device work (CPU)."""
+    import ctypes
+    from sos_amd import _lib
+    L = _lib.lib()
+    w = (ctypes.c_void_p * 65)(*([8] * 65))
+    v = (ctypes.c_uint64 * 65)()
+    assert L.sosx_small_stage(None, 16, 4, w, v, 1, None) == -3                  # no dst
+    assert L.sosx_small_stage(16, None, 4, w, v, 1, None) == -3                  # no src
+    assert L.sosx_small_stage(16, 16, (1 << 20) + 1, w, v, 1, None) == -3        # too large
+    assert L.sosx_small_stage(16, 16, 4, w, v, 0, None) == -3                    # no posts
+    assert L.sosx_small_stage(16, 16, 4, w, v, 65, None) == -3                   # > SOSX_MAX_FOLD
+    assert L.sosx_small_stage(16, 16, 4, None, v, 1, None) == -3
+    assert L.sosx_small_stage(16, 16, 4, w, None, 1, None) == -3
+    z = (ctypes.c_void_p * 2)(8, None)
+    assert L.sosx_small_stage(16, 16, 4, z, v, 2, None) == -3                    # a null word

@@ -376,3 +376,37 @@ def test_small_linear_kernel(torch_cuda, np_, dt, op, layout):
         off = optr - ob.data_ptr()
         got = np.frombuffer(ob[off:off + srcs[0].nbytes].numpy().tobytes(), srcs[0].dtype)
         assert np.array_equal(bits(got), bits(ref)), (np_, dt, op, n, layout)
+
+
+@pytest.mark.parametrize("nwords", [1, 7, 8, 9, 63])
+@pytest.mark.parametrize("src_off,dst_off", [(0, 0), (4, 0), (0, 8), (1, 3)])
+def test_small_stage_kernel(torch_cuda, nwords, src_off, dst_off):
+    """sosx_small_stage (the small path's staging of a device operand): the bytes land in
+    pinned host memory unchanged, at every size and (mis)alignment, and every post word
+    holds its value afterwards -- through the 8-word and the 64-word argument blocks."""
+    import ctypes
+    torch = torch_cuda
+    L = _lib.lib()
+    rng = np.random.default_rng(nwords * 31 + src_off * 7 + dst_off)
+    words = torch.zeros(64 * 8, dtype=torch.int64, pin_memory=True)   # one per 64-B line
+    wptr = [words.data_ptr() + 64 * k for k in range(nwords)]
+    call = 0
+    for nbytes in (1, 15, 16, 4096 + 3, 65536, (1 << 20) - 5):
+        call += 1
+        raw = rng.integers(0, 256, nbytes + 32, dtype=np.uint8)
+        src = torch.from_numpy(raw).cuda()
+        dst = torch.zeros(nbytes + 64, dtype=torch.uint8, pin_memory=True)
+        dbase = (-dst.data_ptr()) % 16 + dst_off
+        vals = [call * 1000 + k for k in range(nwords)]
+        torch.cuda.synchronize()
+        rc = L.sosx_small_stage(ctypes.c_void_p(dst.data_ptr() + dbase),
+                                ctypes.c_void_p(src.data_ptr() + src_off), ctypes.c_size_t(nbytes),
+                                (ctypes.c_void_p * nwords)(*wptr), (ctypes.c_uint64 * nwords)(*vals),
+                                nwords, None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        got = dst[dbase:dbase + nbytes].numpy()
+        assert np.array_equal(got, raw[src_off:src_off + nbytes]), (nbytes, src_off, dst_off)
+        assert int(dst[:dbase].sum()) == 0 and int(dst[dbase + nbytes:].sum()) == 0
+        w = words.view(-1, 8)[:, 0].numpy()
+        assert list(w[:nwords]) == vals and not w[nwords:].any(), nbytes
