@@ -32,11 +32,13 @@
 // itself (steps 1-2 on the device), and the fold kernel, queued behind it, writes the
 // result into the device target directly: one more launch, against the executors'
 // exchange, fold and call-completion wait.  Measured with P PEs on one GPU, fp32 sum under AUTO
-// (profiles/r3_small_latency.txt, run dx): 20 / 23 / 72 us per 4-byte call at P = 2 / 4 /
-// 8 against 40 / 46 / 173 on the p2p executor; the executor wins again from P * bytes =
-// 256 KiB at P = 4 (64 vs 56 us) and 512 KiB at P = 2 (72 vs 49), where the slot traffic
-// over the host link costs more than the exchange saves.  The path takes device operands
-// while P * bytes <= SHMEMX_SMALL_DEVICE (default 128 KiB).
+// (profiles/r3_small_latency.txt, runs dx and dx2): 20-24 / 23-27 / 71-72 us per 4-byte
+// call at P = 2 / 4 / 8 against 40 / 46 / 173 on the p2p executor; from P * bytes =
+// 256 KiB at P = 4 (53-64 vs 56 us) and 512 KiB at P = 2 (72-81 vs 49) the slot traffic
+// over the host link costs as much as the exchange saves, or more.  The path takes device
+// operands while P * bytes <= SHMEMX_SMALL_DEVICE (default 128 KiB).  The GPU-side posts
+// do not shorten the critical path (a peer's fold still launches after the post arrives);
+// they save the host a completion round trip.
 //
 // Slot reuse: each PE alternates between two data slots.  A post to receiver r carries
 // a per-pair index k (posted[q][r] = k) and the slot id (ring[q][r][k % 2]); receiver r
