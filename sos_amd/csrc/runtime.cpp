@@ -537,6 +537,21 @@ bool is_device_ptr(const void *p)
     return a.type == hipMemoryTypeDevice;
 }
 
+bool is_local_device_ptr(const void *p)
+{
+    State &s = st();
+    const char *c = (const char *)p;
+    if (!p) return false;
+    if (s.dev_heap.contains(p, 1) || (s.ext_base && c >= (char *)s.ext_base && c < (char *)s.ext_base + s.ext_size))
+        return true;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice && a.device == s.device;
+}
+
 bool is_symmetric(const void *p, size_t bytes)
 {
     State &s = st();

@@ -155,6 +155,9 @@ void *stage(size_t bytes);
 
 // Is `p` a device (HBM) pointer?  Host pageable, pinned and static data are not.
 bool is_device_ptr(const void *p);
+// HBM of this PE's own GPU (the library's device heaps, or a runtime query): what a kernel
+// on the PE's stream may read without peer access.
+bool is_local_device_ptr(const void *p);
 
 // Symmetric check (SHMEM_ERR_CHECK_SYMMETRIC, src/shmem_internal.h:250-290).
 bool is_symmetric(const void *p, size_t bytes);

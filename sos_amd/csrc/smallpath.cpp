@@ -284,8 +284,12 @@ bool small_path_takes(int alg, const void *target, const void *source, size_t by
 {
     if (!g.ready || bytes == 0 || bytes > g.slot || t.size < 2 || t.size > kMaxPE) return false;
     const size_t team_bytes = (size_t)t.size * bytes;
-    if (is_device_ptr(source) || is_device_ptr(target)) {
+    const bool dev_src = is_device_ptr(source), dev_dst = is_device_ptr(target);
+    if (dev_src || dev_dst) {
+        // the copy and fold kernels touch device operands directly: this GPU's HBM only
         if (team_bytes > g.dev_team_bytes) return false;
+        if ((dev_src && !is_local_device_ptr(source)) || (dev_dst && !is_local_device_ptr(target)))
+            return false;
     } else if (sosplan::is_bcast(alg)) {  // every PE reads one operand, the root's
         if (bytes > kTeamBytes) return false;
     } else if (bytes > kLatencyBytes && team_bytes > kTeamBytes) {
