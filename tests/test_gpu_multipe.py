@@ -112,6 +112,19 @@ def test_team_check_small_path_bytes():
     assert all(int(c) > 0 for _, c in ok), ok
 
 
+@pytest.mark.parametrize("np_", [2, 4, 5])
+def test_small_path_stress(np_):
+    """400 seeded small reductions over interleaved teams (world, even PEs, odd PEs),
+    host-heap and device-heap operands, both sides of the crossover
+    (tests/small_stress_pe.py): the shared-memory slots and per-pair post counters under
+    every reuse order, each result bit for bit against the CPU oracle."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "small_stress_pe.py")], timeout=300)
+    ok = re.findall(r"PE (\d+)/\d+: \d+ checks OK \(small-path calls (\d+), device (\d+)\)", r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _, _ in ok) == list(range(np_)), \
+        r.stdout + r.stderr[-3000:]
+    assert all(int(c) > 0 and int(d) > 0 for _, c, d in ok), ok
+
+
 @pytest.mark.parametrize("np_,signal,small_dev", [(2, "host", True), (3, "host", True),
                                                    (4, "host", False), (8, "host", True),
                                                    (3, "stream", True), (8, "stream", False)])
