@@ -314,3 +314,30 @@ def test_combine_host_pipeline_release_and_regrow(torch_cuda, sos, oracle):
                                  b.ctypes.data_as(ctypes.c_void_p), n, chunk)
         assert rc == 0
         assert same_bits(got, ref), chunk
+
+
+def test_combine_past_2_31_elements(torch_cuda, sos, oracle):
+    """A local combine of 2^31 + 4101 uint8 elements starting 3 bytes past a 16-B
+    boundary (4 GiB of operands): SOS's `int nreduce` stops at 2^31 - 1, this build's
+    size_t count does not, and every index stays 64-bit (the vector tiles, the ragged head
+    and tail).  Inputs from the device generator and the oracle's (bit-identical) one; the
+    expected bytes from the oracle's reduce_local in < 2^31-element slices (an
+    elementwise op, so slicing is exact)."""
+    torch = torch_cuda
+    n, off, dt, op = (1 << 31) + 4101, 3, 18, 5          # uint8 sum (wraps)
+    a = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    b = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    sos.fill(dt, 0, 31, 0, a.data_ptr() + off, n)
+    sos.fill(dt, 0, 31, 1, b.data_ptr() + off, n)
+    torch.cuda.synchronize()
+    sos.combine(op, dt, a.data_ptr() + off, b.data_ptr() + off, n)
+    torch.cuda.synchronize()
+    got = a[off:off + n].cpu().numpy()
+    del a, b
+    exp = oracle.fill(dt, 0, 31, 0, n)
+    step = 1 << 30
+    for s in range(0, n, step):
+        e = min(n, s + step)
+        oracle.reduce_local(op, dt, oracle.fill(dt, 0, 31, 1, e - s, s), exp[s:e])
+    assert np.array_equal(got, exp)
+    assert not np.array_equal(exp[-4101:], oracle.fill(dt, 0, 31, 0, 4101, n - 4101))  # tail combined

@@ -112,6 +112,17 @@ def test_team_check_small_path_bytes():
     assert all(int(c) > 0 for _, c in ok), ok
 
 
+def test_team_reduction_past_2_31_elements():
+    """shmem_uint8_sum_reduce of 2^31 + 4101 elements per PE across 2 PE processes
+    (tests/big_count_pe.py): SOS's int count stops below this, this build's size_t does
+    not; the AUTO ring's chunks, exchange and fold against the oracle's ring, bit for
+    bit.  Device heap 9 GiB per PE: the operands plus the p2p exchange scratch."""
+    r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "big_count_pe.py")], timeout=400,
+               extra_env={"SHMEMX_DEVICE_HEAP_SIZE": "9G", "SHMEMX_STAGE_BYTES": "4200M"})
+    ok = re.findall(r"PE (\d+)/2: \d+ elements OK", r.stdout)
+    assert r.returncode == 0 and sorted(map(int, ok)) == [0, 1], r.stdout + r.stderr[-3000:]
+
+
 @pytest.mark.parametrize("np_", [2, 4, 5])
 def test_small_path_stress(np_):
     """400 seeded small reductions over interleaved teams (world, even PEs, odd PEs),
