@@ -65,7 +65,8 @@ def test_reduce_types_4_pes(examples):
 
 @pytest.mark.parametrize("np_,signal,small_dev", [(2, "stream", True), (3, "stream", False),
                                                    (4, "stream", True), (8, "stream", True),
-                                                   (3, "host", False), (8, "host", False)])
+                                                   (3, "host", False), (8, "host", False),
+                                                   (12, "host", True)])
 def test_team_check(np_, signal, small_dev):
     """Every schedule across np_ PE processes, with the p2p transport's counters moved by
     stream-ordered device signals (the default) or by the host every round
@@ -138,7 +139,8 @@ def test_small_path_stress(np_):
 
 @pytest.mark.parametrize("np_,signal,small_dev", [(2, "host", True), (3, "host", True),
                                                    (4, "host", False), (8, "host", True),
-                                                   (3, "stream", True), (8, "stream", False)])
+                                                   (3, "stream", True), (8, "stream", False),
+                                                   (12, "host", True)])
 def test_coll_check(np_, signal, small_dev):
     """Scans and broadcasts through the public API (tests/coll_check_pe.py), p2p counters
     moved by the host or by stream-ordered device signals; small device operands through
