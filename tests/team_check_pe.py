@@ -183,6 +183,23 @@ def main():
                     checks += 1
                     if mm:
                         bad.append(("perspective", alg, tname, oname, n, mode, mm))
+    # nreduce = 0: every schedule returns at once and leaves the target alone, on the device
+    # and on the host heap (SOS returns before any exchange, src/collectives.c:662, :873)
+    sentinel = np.full(64, 0xA5, np.uint8)
+    for alg in ALGS:
+        S.shmemx_set_reduce_algorithm(L.ALGS[alg])
+        _hip_copy(hdst, sentinel.ctypes.data, 64)
+        S.shmem_float_sum_reduce(world, hdst, hsrc, 0)
+        ctypes.memmove(hh_out, sentinel.ctypes.data, 64)
+        S.shmem_double_max_reduce(world, hh_out, hh_in, 0)
+        back = np.empty(64, np.uint8)
+        _hip_copy(back.ctypes.data, hdst, 64)
+        hh = np.ctypeslib.as_array((ctypes.c_uint8 * 64).from_address(hh_out)).copy()
+        checks += 2
+        if not np.array_equal(back, sentinel):
+            bad.append(("nreduce=0", alg, "device"))
+        if not np.array_equal(hh, sentinel):
+            bad.append(("nreduce=0", alg, "hostheap"))
     S.shmemx_set_reduce_algorithm(L.ALGS["auto"])
     S.shmem_barrier_all()
     S.shmemx_free_device(hdst)
