@@ -66,7 +66,7 @@ def test_reduce_types_4_pes(examples):
 @pytest.mark.parametrize("np_,signal,small_dev", [(2, "stream", True), (3, "stream", False),
                                                    (4, "stream", True), (8, "stream", True),
                                                    (3, "host", False), (8, "host", False),
-                                                   (12, "host", True)])
+                                                   (12, "host", True), (1, "host", False)])
 def test_team_check(np_, signal, small_dev):
     """Every schedule across np_ PE processes, with the p2p transport's counters moved by
     stream-ordered device signals (the default) or by the host every round
@@ -82,10 +82,11 @@ def test_team_check(np_, signal, small_dev):
                     r"device (\d+)\)", r.stdout)
     assert r.returncode == 0 and sorted(int(p) for p, _, _, _ in ok) == list(range(np_)), \
         r.stdout + r.stderr[-3000:]
-    assert {m for _, m, _, _ in ok} == {signal}, ok
+    if np_ > 1:  # one PE has no p2p peers to signal
+        assert {m for _, m, _, _ in ok} == {signal}, ok
     # the host-resident recdbl_sw calls below 64 KiB took the shared-memory path, and the
-    # small device-resident ones did when it was on
-    assert all(int(c) > 0 for _, _, c, _ in ok), ok
+    # small device-resident ones did when it was on (a 1-PE job has no team to meet)
+    assert all((int(c) > 0) == (np_ > 1) for _, _, c, _ in ok), ok
     assert all((int(d) > 0) == small_dev for _, _, _, d in ok), ok
 
 
