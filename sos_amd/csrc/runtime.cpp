@@ -254,7 +254,7 @@ static const EnvDef kEnv[] = {
      "p2p round signalling: stream (device) or host"},
     {"SHMEMX_P2P_TIMEOUT", "long", "300", "device", "Seconds before a p2p wait ends the job"},
     {"SHMEMX_SMALL_HOST", "bool", "true", "device",
-     "Host-resident team reductions of small operands through node shared memory"},
+     "Small team collectives through node shared memory (host operands; device ones too, below)"},
     {"SHMEMX_SMALL_HOST_BYTES", "size", "1048576", "device",
      "Largest operand of that path (its slots: at most 32 MiB over all PEs)"},
     {"SHMEMX_SMALL_DEVICE", "size", "131072", "device",
