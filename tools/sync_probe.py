@@ -16,7 +16,9 @@ def main():
     names = ["hipStreamSynchronize", "hipStreamQuery spin", "hipEventSynchronize",
              "host spin on a flag the kernel stores",
              "one hipStreamQuery, then host spin on the flag",
-             "hipStreamQuery of an idle stream alone (no launch)"]
+             "hipStreamQuery of an idle stream alone (no launch)",
+             "host spin on a flag stored relaxed (no release fence)",
+             "host spin on the flag, 1024-thread workgroup"]
     out = {}
     for _ in range(2):
         for m, name in enumerate(names):

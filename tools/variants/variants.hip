@@ -401,12 +401,20 @@ int sosxv_prefix(int v, void *const *outs, const void *const *ins, int np, size_
 // 1: spin on hipStreamQuery; 2: hipEventRecord + hipEventSynchronize; 3: the kernel
 // stores a flag into pinned host memory (system scope) and the host spins on it; 4: as
 // 3 after one hipStreamQuery of the busy stream; 5: one hipStreamQuery of an idle
-// stream alone (no launch).
+// stream alone (no launch); 6: as 3 with a RELAXED system-scope store (no release fence,
+// so no L2 write-back before it); 7: as 3 from a 1024-thread workgroup (the small path's
+// copy kernel shape).  Modes 3, 4, 6, 7 use a coherent (fine-grained) flag, as the
+// product's completion words.
 // Returns the mean microseconds per launch+wait over `iters`.
 // ---------------------------------------------------------------------------------
 __global__ void k_probe_flag(unsigned *flag, unsigned v)
 {
     if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_probe_flag_relaxed(unsigned *flag, unsigned v)
+{
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #include <chrono>
@@ -415,7 +423,7 @@ extern "C" double sosxv_sync_probe(int mode, int iters, void *stream)
 {
     hipStream_t st = as_stream(stream);
     unsigned *flag = nullptr;
-    if (hipHostMalloc((void **)&flag, 64, hipHostMallocDefault) != hipSuccess) return -1.0;
+    if (hipHostMalloc((void **)&flag, 64, hipHostMallocCoherent) != hipSuccess) return -1.0;
     *flag = 0;
     hipEvent_t ev;
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1.0;
@@ -423,7 +431,10 @@ extern "C" double sosxv_sync_probe(int mode, int iters, void *stream)
     for (int it = -10; it < iters; ++it) {
         const auto t0 = std::chrono::steady_clock::now();
         const unsigned v = (unsigned)(it + 11);
-        hipLaunchKernelGGL(k_probe_flag, dim3(1), dim3(64), 0, st, flag, v);
+        if (mode == 6)
+            hipLaunchKernelGGL(k_probe_flag_relaxed, dim3(1), dim3(64), 0, st, flag, v);
+        else
+            hipLaunchKernelGGL(k_probe_flag, dim3(1), dim3(mode == 7 ? 1024 : 64), 0, st, flag, v);
         if (mode == 0) (void)hipStreamSynchronize(st);
         else if (mode == 1) { while (hipStreamQuery(st) == hipErrorNotReady) {} }
         else if (mode == 2) { (void)hipEventRecord(ev, st); (void)hipEventSynchronize(ev); }
