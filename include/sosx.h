@@ -184,11 +184,6 @@ int sosx_count_mismatch(const void *a, const void *b, size_t count, size_t elem_
 /* Synchronous copy between any host/device addresses (hipMemcpyDefault semantics). */
 int sosx_memcpy(void *dst, const void *src, size_t bytes, void *stream);
 
-/* Store `value` into *word (pinned host memory, device-visible) after all earlier work
- * on `stream` has finished: a completion mark the host polls instead of synchronising
- * the stream. */
-int sosx_stream_mark(uint32_t *word, uint32_t value, void *stream);
-
 /* Multi-segment copy in one launch (peer-to-peer transport gathers). */
 int sosx_gather(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,
                 void *stream);

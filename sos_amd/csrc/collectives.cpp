@@ -521,12 +521,9 @@ void execute(int alg, void *target, const void *source, size_t count, size_t ts,
         if (ncclAllReduce(dsrc, ddst, count, ar_ty, ar_op, s.comm, s.stream) != ncclSuccess)
             raise_error("%s: %s", fn, status_text(SOSX_ERR_RCCL));
         if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, true), s.stream);
-        if (!dev_dst) {
+        if (!dev_dst)
             hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
-            hip_check(hipStreamSynchronize(s.stream), fn);
-        } else {
-            hip_check(stream_wait(s.stream), fn);
-        }
+        hip_check(hipStreamSynchronize(s.stream), fn);
         if (g_prof.on) g_prof.collect();
         return;
     }
@@ -538,12 +535,9 @@ void execute(int alg, void *target, const void *source, size_t count, size_t ts,
     if (g_prof.on) g_prof.ncall++;
     rc = exec_rccl(p, t, b, op, dt, s.stream);
     if (rc) raise_error("%s: %s", fn, status_text(rc));
-    if (!dev_dst && p.writes_dst) {  // the target may be pageable: a full synchronisation
+    if (!dev_dst && p.writes_dst)
         hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
-        hip_check(hipStreamSynchronize(s.stream), fn);
-    } else {
-        hip_check(stream_wait(s.stream), fn);
-    }
+    hip_check(hipStreamSynchronize(s.stream), fn);
     if (g_prof.on) g_prof.collect();
 }
 
@@ -575,7 +569,7 @@ void op_to_all(void *target, const void *source, size_t count, size_t ts, const 
     // small operands (recdbl_sw below the crossover, the ring above it; host-resident, or
     // device-resident below SHMEMX_SMALL_DEVICE): through the node shared segment, one
     // kernel reading every PE's operand in place (smallpath.cpp), no DMA copies
-    if (!s.rccl_allreduce && small_path_takes(alg, target, source, bytes, t)) {
+    if (small_path_route(alg, target, source, bytes, t, !s.rccl_allreduce, fn)) {
         small_path_reduce(alg, target, source, count, ts, t, op, dt, fn);
         return;
     }
@@ -699,7 +693,7 @@ int sos_api_broadcast(shmem_team_t team, void *dest, const void *source, size_t 
     if (bytes == 0) return 0;
     // the team forms copy source to dest on the root as well (collectives_c.c4:390-397)
     const int plan = sosplan::bcast_alg(PE_root, true);
-    if (t->size > 1 && small_path_takes(plan, dest, source, bytes, *t)) {
+    if (t->size > 1 && small_path_route(plan, dest, source, bytes, *t, true, fn)) {
         small_path_reduce(plan, dest, source, nelems, type_size, *t, SOSX_OP_SUM, SOSX_DT_UCHAR, fn);
         return 0;
     }
@@ -729,7 +723,7 @@ static void bcast_active_set(void *target, const void *source, size_t nlong, siz
     t.valid = true;
     // the root's target is not written (collectives_c.c4:342-378)
     const int plan = sosplan::bcast_alg(PE_root, false);
-    if (small_path_takes(plan, target, source, bytes, t)) {
+    if (small_path_route(plan, target, source, bytes, t, true, fn)) {
         small_path_reduce(plan, target, source, nlong, ts, t, SOSX_OP_SUM, SOSX_DT_UCHAR, fn);
         return;
     }
@@ -780,7 +774,7 @@ int sos_api_scan(shmem_team_t team, void *dest, const void *source, size_t nelem
     if (t->size > sosplan::PLAN_MAX_PE)
         raise_error("%s: teams of more than %d PEs are not supported", fn, sosplan::PLAN_MAX_PE);
     const int plan = exclusive ? sosplan::PLAN_EXSCAN : sosplan::PLAN_INSCAN;
-    if (t->size > 1 && small_path_takes(plan, dest, source, bytes, *t)) {
+    if (t->size > 1 && small_path_route(plan, dest, source, bytes, *t, true, fn)) {
         // small operands: one kernel per PE over node shared memory (smallpath.cpp)
         small_path_reduce(plan, dest, source, nelems, type_size, *t, op, datatype, fn);
         return 0;

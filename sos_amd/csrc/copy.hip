@@ -65,15 +65,6 @@ using SigArgs = Sig<kMaxSig>;
 
 __global__ __launch_bounds__(kMaxSig) void k_p2p_signal(SigArgs a) { sig_step(a, threadIdx.x); }
 
-// Completion mark (sosrt::stream_wait): runs after everything queued before it on the
-// stream; its system-scope release store also writes back any dirty L2 lines of the
-// earlier kernels, so what they wrote to host memory is visible once the host sees it.
-__global__ void k_stream_mark(uint32_t *word, uint32_t v)
-{
-    if (threadIdx.x == 0) __hip_atomic_store(word, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-
 struct GatherArgs {
     const char *src[kMaxSeg];
     char *dst[kMaxSeg];
@@ -251,15 +242,6 @@ int sosx_gather_signalled(int nseg, const void *const *srcs, void *const *dsts,
     gate.err = err;
     gate.limit = limit_ticks;
     return gather_impl(nseg, srcs, dsts, bytes, &gate, as_stream(stream));
-}
-
-// Store `value` into *word (pinned host memory) once all earlier work on `stream` is
-// done (stream order).  The host then learns of completion by polling the word.
-int sosx_stream_mark(uint32_t *word, uint32_t value, void *stream)
-{
-    if (!word) return SOSX_ERR_ARG;
-    hipLaunchKernelGGL(k_stream_mark, dim3(1), dim3(64), 0, as_stream(stream), word, value);
-    return hip_ok(hipGetLastError());
 }
 
 // One signalling step of the p2p transport on `stream`: store vals[i] to waddr[i]

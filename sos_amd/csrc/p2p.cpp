@@ -126,8 +126,11 @@ template <class X> X *dev(X *host)
 // Test hook (tests/test_gpu_multipe.py::test_p2p_stall_mid_call): the PE named by
 // SOSX_P2P_TEST_STALL_PE stops for 60 s right after the entry boundary of its first
 // multi-round call, so its peers meet the bounded DEVICE waits of the later rounds.
+// Compiled into the test build of the library only (-DSOSX_TEST_HOOKS,
+// tests/fakerccl/libsos_amd_fakerccl.so); a no-op in the product.
 void stall_hook()
 {
+#ifdef SOSX_TEST_HOOKS
     static const int pe = [] {
         const char *e = getenv("SOSX_P2P_TEST_STALL_PE");
         return e && *e ? atoi(e) : -1;
@@ -138,6 +141,7 @@ void stall_hook()
         fprintf(stderr, "[%04d] test hook: stalling 60 s after the call's entry boundary\n", pe);
         sleep(60);
     }
+#endif
 }
 
 double wait_limit_s()
@@ -429,7 +433,7 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
             first_xfer_round = false;
             bool sends = false;
             for (const auto &x : r.xfers) sends |= x.send != 0;
-            if (sends && stream_wait(stream) != hipSuccess) return SOSX_ERR_HIP;
+            if (sends && hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
             host_flush();
             stall_hook();
         } else {
@@ -530,7 +534,7 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
     }
     // the exit boundary (the last round's consumed marks) on the host, after the sync
     phase(PH_ENQUEUE);
-    const hipError_t e = stream_wait(stream);
+    const hipError_t e = hipStreamSynchronize(stream);
     if (__atomic_load_n(&sh->sig_err[my_world], __ATOMIC_ACQUIRE))
         raise_error("p2p transport: timed out after %.0f s waiting for a peer (device wait)",
                     wait_limit_s());
@@ -687,7 +691,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
         bool any_send = false;
         for (const auto &x : r.xfers) any_send |= x.send != 0;
         if (any_send) {
-            if (stream_wait(stream) != hipSuccess) return SOSX_ERR_HIP;
+            if (hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
             phase(PH_SYNC_SEND);
             for (const auto &x : r.xfers)
                 if (x.send) {
@@ -757,7 +761,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
         // 4. receives done -> consumed; wait for my sends to be consumed
         phase(PH_ENQUEUE);
         if (!segs.empty() || fuse_ok) {
-            if (stream_wait(stream) != hipSuccess) return SOSX_ERR_HIP;
+            if (hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
         }
         phase(PH_SYNC_OPS);
         for (auto &sg : segs) sh->consumed[sg.peer_world][my_world].fetch_add(1, std::memory_order_release);
@@ -772,7 +776,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
             if (rc) return rc;
         }
     }
-    const hipError_t e = stream_wait(stream);
+    const hipError_t e = hipStreamSynchronize(stream);
     phase(PH_SYNC_END);
     if (tr && ++g_trace.calls % g_trace.every == 0) {  // window averages, then reset
         const double k = 1e6 / (double)g_trace.every;

@@ -111,65 +111,6 @@ void hip_check(hipError_t e, const char *what)
     if (e != hipSuccess) raise_error("HIP error in %s: %s", what, hipGetErrorString(e));
 }
 
-// Completion marks for stream_wait: a ring of words in pinned, coherent host memory.
-// Each wait takes the next word and a fresh value, so concurrent waits (threads on
-// different teams) never share a word unless 64 are in flight at once.
-namespace {
-constexpr unsigned kMarkWords = 64;
-std::atomic<uint32_t *> g_marks{nullptr};
-std::atomic<uint32_t> g_mark_seq{0};
-
-double mono_s()
-{
-    timespec ts;
-    clock_gettime(CLOCK_MONOTONIC, &ts);
-    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
-}
-}  // namespace
-
-hipError_t stream_wait(hipStream_t stream)
-{
-    uint32_t *marks = g_marks.load(std::memory_order_acquire);
-    if (!marks) {
-        static std::mutex mu;
-        std::lock_guard<std::mutex> lk(mu);
-        marks = g_marks.load(std::memory_order_acquire);
-        if (!marks) {
-            uint32_t *m = nullptr;
-            if (hipHostMalloc((void **)&m, kMarkWords * 64, hipHostMallocCoherent) != hipSuccess) {
-                (void)hipGetLastError();
-                return hipStreamSynchronize(stream);
-            }
-            memset(m, 0, kMarkWords * 64);
-            g_marks.store(m, std::memory_order_release);
-            marks = m;
-        }
-    }
-    // nothing queued (e.g. a call's entry boundary): no mark to wait for
-    const hipError_t q = hipStreamQuery(stream);
-    if (q != hipErrorNotReady) return q;
-    uint32_t v = ++g_mark_seq;
-    if (v == 0) v = ++g_mark_seq;
-    uint32_t *word = marks + (v % kMarkWords) * 16;  // one 64-B line per word
-    if (sosx_stream_mark(word, v, stream) != SOSX_OK) return hipStreamSynchronize(stream);
-    unsigned spins = 0;
-    double t0 = 0;
-    while (__atomic_load_n(word, __ATOMIC_ACQUIRE) != v) {
-        __builtin_ia32_pause();
-        if ((++spins & 0x3FFF) != 0) continue;
-        // every ~16k polls: a faulted or drained stream ends the wait; a long one (a
-        // large exchange) stops polling after 10 ms and leaves the rest to the runtime
-        const hipError_t e = hipStreamQuery(stream);
-        if (e != hipErrorNotReady) {
-            if (e != hipSuccess) return e;
-            return __atomic_load_n(word, __ATOMIC_ACQUIRE) == v ? hipSuccess : hipStreamSynchronize(stream);
-        }
-        if (t0 == 0) t0 = mono_s();
-        else if (mono_s() - t0 > 0.01) return hipStreamSynchronize(stream);
-    }
-    return hipSuccess;
-}
-
 void nccl_check(ncclResult_t r, const char *what)
 {
     if (r != ncclSuccess) raise_error("RCCL error in %s: %s", what, ncclGetErrorString(r));

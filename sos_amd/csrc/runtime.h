@@ -141,12 +141,6 @@ void check_initialized(const char *fn);
 size_t env_size(const char *name, size_t dflt);
 void hip_check(hipError_t e, const char *what);
 
-// Wait until all work queued on `st` has finished, as hipStreamSynchronize does, by
-// polling a completion mark in pinned host memory (sosx_stream_mark): about 5 us less
-// per wait (profiles/r3_sync_probe.json).  Errors as hipStreamSynchronize reports them.
-// Not for streams with pending copies to PAGEABLE host memory (the runtime finishes
-// those on the host).
-hipError_t stream_wait(hipStream_t st);
 void nccl_check(ncclResult_t r, const char *what);
 
 // Device workspaces (grown, never shrunk).
@@ -193,6 +187,10 @@ size_t small_shared_bytes(int npes);
 void small_path_setup(void *region, size_t bytes);   // collective (init_common)
 void small_path_teardown();
 bool small_path_takes(int alg, const void *target, const void *source, size_t bytes, const Team &t);
+// small_path_takes (when `allowed`) for one team call, published to the team and checked
+// against every peer's choice: a disagreement ends the job with both PEs' operands named.
+bool small_path_route(int alg, const void *target, const void *source, size_t bytes, const Team &t,
+                      bool allowed, const char *fn);
 void small_path_reduce(int alg, void *target, const void *source, size_t count, size_t ts,
                        const Team &t, int op, int dt, const char *fn);
 long small_path_calls();

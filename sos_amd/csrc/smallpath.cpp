@@ -98,8 +98,13 @@ struct alignas(64) PairWord {
 struct SmallCtl {
     PairWord posted[kMaxPE];      // [r]: posts q made for r (count)
     PairWord consumed[kMaxPE];    // [s]: posts from s that q has read (count)
+    PairWord route[kMaxPE];       // [r]: (k << 8) | tag of q's k-th routed call with r
     uint32_t ring[kMaxPE][2];     // [r][k % 2]: data slot of q's k-th post for r
 };
+
+// Route tags (the low byte of a route word): which path a PE took for a call, and the
+// residency of its operands, so that a disagreement names both PEs' operands.
+constexpr uint64_t kRouteSmall = 1, kRouteDevSrc = 2, kRouteDevDst = 4;
 
 struct Small {
     bool ready = false;          // every PE registered the region (agreed at init)
@@ -116,6 +121,9 @@ struct Small {
     void *out = nullptr;         // pinned result slot (hipHostMalloc, device-mapped)
     uint32_t *flags = nullptr;   // per-workgroup completion words (pinned, coherent)
     uint32_t fseq = 0;           // the value the current launch's workgroups store
+    uint64_t routed[kMaxPE] = {0};  // routed calls shared with each world PE (both count)
+    uint64_t route_k[kMaxPE] = {0};  // this call's index with each team peer (small path)
+    uint64_t route_tag = 0;          // this call's route tag
     size_t dev_team_bytes = 0;   // device operands: P * bytes limit (0: host operands only)
     long calls = 0;
     long dev_calls = 0;          // of which with a device operand
@@ -272,19 +280,33 @@ void small_path_teardown()
 long small_path_calls() { return g.calls; }
 long small_path_device_calls() { return g.dev_calls; }
 
+// Collective over the world when the job is up: every PE passes the same limit (checked
+// through the bootstrap), so the path choice for device operands stays uniform.
 size_t small_path_set_device_bytes(size_t team_bytes)
 {
+    State &s = st();
+    if (s.initialized && s.hub.up && s.n_pes > 1) {
+        std::vector<uint64_t> all((size_t)s.n_pes);
+        const uint64_t mine = team_bytes;
+        if (sosboot::hub_allgather(&s.hub, &mine, sizeof(mine), all.data()) != 0)
+            raise_error("sosx_set_small_device_bytes: agreement failed");
+        for (int q = 0; q < s.n_pes; ++q)
+            if (all[(size_t)q] != mine)
+                raise_error("sosx_set_small_device_bytes: PE %d passed %llu, PE %d passed %llu (the call "
+                            "is collective: every PE passes the same limit)", s.my_pe,
+                            (unsigned long long)mine, q, (unsigned long long)all[(size_t)q]);
+    }
     const size_t prev = g.dev_team_bytes;
     g.dev_team_bytes = team_bytes;
     return prev;
 }
 
-// Does a reduction of `bytes` with these operands over team t take the small path?
-bool small_path_takes(int alg, const void *target, const void *source, size_t bytes, const Team &t)
+namespace {
+bool takes(int alg, const void *target, const void *source, size_t bytes, const Team &t, bool dev_src,
+           bool dev_dst)
 {
     if (!g.ready || bytes == 0 || bytes > g.slot || t.size < 2 || t.size > kMaxPE) return false;
     const size_t team_bytes = (size_t)t.size * bytes;
-    const bool dev_src = is_device_ptr(source), dev_dst = is_device_ptr(target);
     if (dev_src || dev_dst) {
         // the copy and fold kernels touch device operands directly: this GPU's HBM only
         if (team_bytes > g.dev_team_bytes) return false;
@@ -302,6 +324,100 @@ bool small_path_takes(int alg, const void *target, const void *source, size_t by
         return false;
     }
     return sosplan::pow2_floor(t.size) <= SOSX_MAX_FOLD;
+}
+}  // namespace
+
+// Does a reduction of `bytes` with these operands over team t take the small path?
+bool small_path_takes(int alg, const void *target, const void *source, size_t bytes, const Team &t)
+{
+    if (!g.ready || bytes == 0 || bytes > g.slot || t.size < 2 || t.size > kMaxPE) return false;
+    return takes(alg, target, source, bytes, t, is_device_ptr(source), is_device_ptr(target));
+}
+
+namespace {
+
+const char *route_text(uint64_t tag)
+{
+    return (tag & kRouteSmall) ? "small shared-memory path" : "executor";
+}
+
+[[noreturn]] void route_mismatch(const char *fn, uint64_t mine, int q, uint64_t theirs, bool known)
+{
+    char other[160];
+    if (known)
+        snprintf(other, sizeof(other), "PE %d the %s (source %s, target %s)", q, route_text(theirs),
+                 (theirs & kRouteDevSrc) ? "device" : "host", (theirs & kRouteDevDst) ? "device" : "host");
+    else
+        snprintf(other, sizeof(other), "PE %d the executor (it finished the call without posting)", q);
+    raise_error("%s: the PEs of a team took different paths for the same call: PE %d the %s "
+                "(source %s, target %s), %s.  Every PE of the team must pass operands of the same "
+                "residency, and SHMEMX_SMALL_DEVICE / sosx_set_small_device_bytes must agree",
+                fn, st().my_pe, route_text(mine), (mine & kRouteDevSrc) ? "device" : "host",
+                (mine & kRouteDevDst) ? "device" : "host", other);
+}
+
+// Wait for peer q's k-th post of a small-path call (kp), checking q's route word: a
+// peer that took the executor for this call (its route word for the call says so, or it
+// has moved past the call without posting) ends the job at once with both PEs' operands
+// named, instead of after SHMEMX_P2P_TIMEOUT.
+void wait_post(int q, uint64_t kp, uint64_t mine, const char *fn)
+{
+    const int mw = st().my_pe;
+    const std::atomic<uint64_t> &w = ctl(q)->posted[mw].v;
+    if (w.load(std::memory_order_acquire) >= kp) return;
+    const double t0 = now_s();
+    double past = 0;  // when q was first seen past the call with the post missing
+    unsigned spins = 0;
+    while (w.load(std::memory_order_acquire) < kp) {
+        __builtin_ia32_pause();
+        if ((++spins & 0xFF) != 0) continue;
+        const uint64_t v = ctl(q)->route[mw].v.load(std::memory_order_acquire);
+        const uint64_t ik = v >> 8, rk = g.route_k[q];
+        if (ik == rk && !(v & kRouteSmall)) route_mismatch(fn, mine, q, v & 0xFF, true);
+        if (ik > rk && w.load(std::memory_order_acquire) < kp) {
+            // q finished this call: on the small path its post came first (a device post
+            // is stored by the copy kernel before q's fold can finish); allow the write
+            // 10 ms to arrive before calling it a disagreement
+            if (past == 0) past = now_s();
+            else if (now_s() - past > 0.01) route_mismatch(fn, mine, q, 0, false);
+        }
+        if ((spins & 0xFFFF) == 0 && now_s() - t0 > limit_s())
+            raise_error("small shared-memory path: timed out after %.0f s waiting for a peer's operand",
+                        limit_s());
+    }
+}
+
+}  // namespace
+
+// Pick the small path or the executor for one team call and publish the choice to the
+// team (route words in node shared memory): SOS's schedule choice depends only on the
+// call's size (src/shmem_collectives.h:179-200), so all PEs agree by construction; this
+// build's choice also depends on each PE's operand residency, so it is verified.  A PE
+// on the small path waits for every peer's post (broadcasts included), and while it
+// waits it reads the peer's route word (wait_post): a peer on the executor ends the job
+// at once, with both PEs' operands named -- the executor PEs, blocked in the exchange,
+// are then reaped by the launcher.  So a disagreement is always seen by a small-path PE,
+// and the executor path pays one store per peer, no wait.  Every team call that can take
+// the small path goes through here on every member PE, so the per-pair counts agree.
+bool small_path_route(int alg, const void *target, const void *source, size_t bytes, const Team &t,
+                      bool allowed, const char *fn)
+{
+    if (!g.ready || t.size < 2 || t.size > kMaxPE || t.my_idx < 0)
+        return allowed && small_path_takes(alg, target, source, bytes, t);
+    const bool dev_src = is_device_ptr(source), dev_dst = target == source ? dev_src : is_device_ptr(target);
+    const bool take = allowed && takes(alg, target, source, bytes, t, dev_src, dev_dst);
+    const int mw = st().my_pe;
+    const uint64_t tag = (take ? kRouteSmall : 0) | (dev_src ? kRouteDevSrc : 0) | (dev_dst ? kRouteDevDst : 0);
+    SmallCtl *mine = ctl(mw);
+    for (int i = 0; i < t.size; ++i) {
+        if (i == t.my_idx) continue;
+        const int r = t.world_rank(i);
+        const uint64_t k = ++g.routed[r];
+        g.route_k[r] = k;
+        mine->route[r].v.store(k << 8 | tag, std::memory_order_release);
+    }
+    g.route_tag = tag;
+    return take;
 }
 
 // recdbl_sw's (or, for alg RING, the ring's; for the scan plans, the scan's) value for
@@ -369,7 +485,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
             continue;
         }
         const uint64_t k = ++g.seen_from[q];
-        wait_ge(ctl(q)->posted[mw].v, k, "a peer's operand");
+        wait_post(q, k, g.route_tag, fn);
         const int qs = (int)ctl(q)->ring[mw][k % 2];
         in[i] = g.dev + slot_off(q, qs);
         from[i] = q;
@@ -422,6 +538,9 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         rc = sosx_small_fold(op, dt, out, leaves, extras, p2, count, g.flags, g.fseq, &nblocks, s.stream);
     }
     if (rc) raise_error("%s: small-path reduction failed (status %d)", fn, rc);
+    // no fold launch followed the copy kernel (an active-set broadcast's root, exscan's
+    // PE 0 with a host target): the call must not return while it still reads `source`
+    if (staged && nblocks == 0) hip_check(hipStreamSynchronize(s.stream), fn);
     phase(3);
     // 4. completion from the workgroups' flags (no stream synchronisation); then the
     //    peers' slots are read: acknowledge; my result out

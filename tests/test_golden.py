@@ -43,35 +43,24 @@ def test_oracle_reproduces_golden():
 
 
 @pytest.mark.gpu
-def test_gpu_reproduces_golden(torch_cuda, sos):
-    from sos_amd import shmem as S
-    torch = torch_cuda
-    ESZ = {4: 4, 11: 8, 23: 4, 24: 8, 27: 16}
-    bad = []
-    for c in CASES:
-        dt, op, n, P = c["type"], c["op"], c["n"], c["P"]
-        es = ESZ[dt]
-        dist = 1 if op == 6 else 0
-        npe = 2 if c["kind"] == "combine" else P
-        src = []
-        for pe in range(npe):
-            t = torch.empty(n * es, dtype=torch.uint8, device="cuda")
-            sos.fill(dt, dist, SEED, pe, t.data_ptr(), n)
-            src.append(t)
-        torch.cuda.synchronize()
-        if [sha(t.cpu().numpy().tobytes()) for t in src] != c["in_sha256"]:
-            bad.append(("inputs", c["kind"], dt, op, n, P))
-            continue
-        if c["kind"] == "combine":
-            sos.combine(op, dt, src[0].data_ptr(), src[1].data_ptr(), n)
-            outs = [src[0]]
-        else:
-            outs = [torch.zeros_like(t) for t in src]
-            S.loopback_allreduce(c["kind"], op, dt, [t.data_ptr() for t in src],
-                                 [t.data_ptr() for t in outs], n)
-        torch.cuda.synchronize()
-        got = [sha(t.cpu().numpy().tobytes()) for t in outs]
-        if got != c["out_sha256"]:
-            bad.append((c["kind"], dt, op, n, P))
-    assert not bad, f"{len(bad)} of {len(CASES)} golden cases differ: {bad[:10]}"
+@pytest.mark.parametrize("config", ["#2", "#3", "#4", "#5"])
+def test_gpu_reproduces_golden(torch_cuda, sos, config):
+    """One test per BASELINE config, so a failure names the config it broke."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import golden_gpu
+    cases = [c for c in CASES if c["config"] == config]
+    bad = golden_gpu.run_cases(torch_cuda, sos, cases, SEED)
+    assert not bad, f"{len(bad)} of {len(cases)} golden cases of {config} differ: {bad[:10]}"
     _ = np
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [1, 2, 4, 8])
+def test_gpu_pi_reduce_known_answer(torch_cuda, sos, P):
+    """BASELINE config #1: examples/pi_reduce.c's golden line per PE count, with its two
+    long long sum reductions through the GPU loopback recdbl_sw."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import golden_gpu
+    assert golden_gpu.pi_lines_gpu(torch_cuda, P) == [golden_gpu.GOLDEN_PI[P]] * P

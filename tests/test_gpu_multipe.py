@@ -185,15 +185,46 @@ def test_small_path_wait_is_bounded(mode):
     assert time.monotonic() - t0 < 55, "the job outlived the late PE's sleep"
 
 
+def test_route_mismatch_ends_the_job_at_once():
+    """PE 0 with host-heap operands (small path), PE 1 with device-heap operands above
+    SHMEMX_SMALL_DEVICE (executor) in the same call: the small-path PE reads the peer's
+    route word while it waits for its post and ends the job with both residencies named,
+    long before SHMEMX_P2P_TIMEOUT (60 s here)."""
+    r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "route_mismatch_pe.py")], timeout=150,
+               extra_env={"SHMEMX_P2P_TIMEOUT": "60", "SHMEMX_SMALL_DEVICE": "16K"})
+    t_end = time.time()
+    assert r.returncode != 0, r.stdout
+    assert "reduction returned" not in r.stdout
+    msg = [ln for ln in r.stderr.splitlines() if "took different paths" in ln]
+    assert msg, r.stderr[-2000:]
+    assert "PE 0 the small shared-memory path (source host, target host)" in msg[0], msg
+    assert "PE 1 the executor (source device, target device)" in msg[0], msg
+    starts = [float(x) for x in re.findall(r"call starts at ([\d.]+)", r.stdout)]
+    assert len(starts) == 2, r.stdout
+    assert t_end - max(starts) < 10, t_end - max(starts)  # teardown included; 60 s if missed
+
+
+def test_small_device_setter_is_collective():
+    """sosx_set_small_device_bytes with different limits on two PEs is refused."""
+    r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "route_mismatch_pe.py"), "setter"],
+               timeout=120)
+    assert r.returncode != 0, r.stdout
+    assert "every PE passes the same limit" in r.stderr, r.stderr[-2000:]
+
+
 def test_p2p_stall_mid_call_costs_one_timeout():
     """A peer that stops after a call's entry boundary (test hook SOSX_P2P_TEST_STALL_PE):
     the waiting PEs' device waits time out in the call's first device step, and the
     call's two later device steps give up at once instead of each waiting out
     SHMEMX_P2P_TIMEOUT again (one timeout per call, not one per step)."""
     T = 5
+    # the hook is compiled into the test build only (the fakerccl twin of the library,
+    # here on the p2p transport, so its RCCL stand-in is never called)
     r = oshrun(4, [sys.executable, os.path.join(ROOT, "tests", "p2p_stall_pe.py")], timeout=150,
                extra_env={"SHMEMX_P2P_TIMEOUT": str(T), "SHMEMX_P2P_SIGNAL": "stream",
-                          "SOSX_P2P_TEST_STALL_PE": "1"})
+                          "SOSX_P2P_TEST_STALL_PE": "1",
+                          "SOSX_LIBRARY": os.path.join(ROOT, "tests", "fakerccl",
+                                                       "libsos_amd_fakerccl.so")})
     t_end = time.time()
     assert r.returncode != 0, r.stdout
     assert "timed out" in r.stderr and "device wait" in r.stderr, r.stderr[-2000:]
