@@ -13,22 +13,12 @@
 
 namespace sos {
 
-template <class T, class OP, int NP, int ORDER>
-__global__ __launch_bounds__(kThreads) void k_fold_scalar(T *out, FoldPtrs ins,
-                                                            size_t n)
-{
-    const size_t stride = (size_t)gridDim.x * kThreads;
-    for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
-        T v[NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) v[k] = ((const T *)ins.p[k])[i];
-        out[i] = fold_elem<T, OP, NP, ORDER>(v);
-    }
-}
-
-// Runtime P (9..64 PEs per team: several PEs per GPU or more than one node): element
-// loads; the TREE order walks the recdbl_sw leaves left to right with a binary-counter
-// stack (merge equal-height neighbours: w[k] = w[k] OP w[k+d]), so no P-sized array.
+// Runtime P, element loads: teams of 9..64 PEs (several PEs per GPU or more than one
+// node), and every fold whose inputs are small (latency-bound: one element per lane) or
+// not 16-B congruent.  The TREE order walks the recdbl_sw leaves left to right with a
+// binary-counter stack (merge equal-height neighbours: w[k] = w[k] OP w[k+d]), so no
+// P-sized array; for P <= 8 it is fold_elem's tree, operation for operation (the extras
+// first, then distance 1, 2, 4 pairs with the lower subtree the left operand).
 template <class T, class OP, int ORDER>
 __global__ __launch_bounds__(kThreads) void k_fold_dyn(T *out, FoldPtrs ins, int np,
                                                          size_t n)
@@ -102,19 +92,23 @@ namespace {
 // flight at once instead of one workgroup's; latency, not bandwidth, bounds these calls.
 constexpr size_t kSpreadBytes = 64 * 1024;
 
+template <class T, class OP, int ORDER>
+int launch_fold_dyn(T *out, const FoldPtrs &ins, int np, size_t n, hipStream_t st)
+{
+    size_t blocks = (n + kThreads - 1) / kThreads;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL((k_fold_dyn<T, OP, ORDER>), dim3((unsigned)blocks), dim3(kThreads), 0, st, out, ins,
+                       np, n);
+    return hip_ok(hipGetLastError());
+}
+
 template <class T, class OP, int NP, int ORDER>
 int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 {
     uintptr_t o = (uintptr_t)out;
     bool congruent = (o % sizeof(T)) == 0 && sizeof(T) <= 16;
     for (int k = 0; k < NP; ++k) congruent &= (((uintptr_t)ins.p[k] ^ o) & 15) == 0;
-    if (!congruent || n * sizeof(T) <= kSpreadBytes) {
-        size_t blocks = (n + kThreads - 1) / kThreads;
-        if (blocks > 8192) blocks = 8192;
-        hipLaunchKernelGGL((k_fold_scalar<T, OP, NP, ORDER>), dim3((unsigned)blocks),
-                           dim3(kThreads), 0, st, out, ins, n);
-        return hip_ok(hipGetLastError());
-    }
+    if (!congruent || n * sizeof(T) <= kSpreadBytes) return launch_fold_dyn<T, OP, ORDER>(out, ins, NP, n, st);
     constexpr int U = NP <= 2 ? 4 : (NP <= 4 ? 2 : 1);
     Geom g = make_geom(o, n, sizeof(T), U);
     hipLaunchKernelGGL((k_fold<T, OP, NP, ORDER, U>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
@@ -133,13 +127,7 @@ int launch_fold(T *out, const FoldPtrs &ins, int nin, size_t n, hipStream_t st)
         case 6: return launch_fold_np<T, OP, 6, ORDER>(out, ins, n, st);
         case 7: return launch_fold_np<T, OP, 7, ORDER>(out, ins, n, st);
         case 8: return launch_fold_np<T, OP, 8, ORDER>(out, ins, n, st);
-        default: {
-            size_t blocks = (n + kThreads - 1) / kThreads;
-            if (blocks > 8192) blocks = 8192;
-            hipLaunchKernelGGL((k_fold_dyn<T, OP, ORDER>), dim3((unsigned)blocks), dim3(kThreads), 0,
-                               st, out, ins, nin, n);
-            return hip_ok(hipGetLastError());
-        }
+        default: return launch_fold_dyn<T, OP, ORDER>(out, ins, nin, n, st);
     }
 }
 
@@ -169,17 +157,21 @@ struct PrefixFn {
         bool congruent = (o % sizeof(T)) == 0 && sizeof(T) <= 16;
         for (int k = 0; k < np; ++k)
             congruent &= (((uintptr_t)p->in[k] ^ o) & 15) == 0 && (((uintptr_t)p->out[k] ^ o) & 15) == 0;
-        if (congruent) {
-            switch (np) {
-                case 1: return launch_prefix_np<T, OP, 1>(*p, n, st);
-                case 2: return launch_prefix_np<T, OP, 2>(*p, n, st);
-                case 3: return launch_prefix_np<T, OP, 3>(*p, n, st);
-                case 4: return launch_prefix_np<T, OP, 4>(*p, n, st);
-                case 5: return launch_prefix_np<T, OP, 5>(*p, n, st);
-                case 6: return launch_prefix_np<T, OP, 6>(*p, n, st);
-                case 7: return launch_prefix_np<T, OP, 7>(*p, n, st);
-                case 8: return launch_prefix_np<T, OP, 8>(*p, n, st);
-                default: break;
+        // the vector kernels serve the team scans, which are sums (shmemx_<T>_sum_inscan /
+        // _exscan); other ops take the element loop (sosx_prefix accepts them all)
+        if constexpr (std::is_same<OP, OpSum>::value) {
+            if (congruent) {
+                switch (np) {
+                    case 1: return launch_prefix_np<T, OP, 1>(*p, n, st);
+                    case 2: return launch_prefix_np<T, OP, 2>(*p, n, st);
+                    case 3: return launch_prefix_np<T, OP, 3>(*p, n, st);
+                    case 4: return launch_prefix_np<T, OP, 4>(*p, n, st);
+                    case 5: return launch_prefix_np<T, OP, 5>(*p, n, st);
+                    case 6: return launch_prefix_np<T, OP, 6>(*p, n, st);
+                    case 7: return launch_prefix_np<T, OP, 7>(*p, n, st);
+                    case 8: return launch_prefix_np<T, OP, 8>(*p, n, st);
+                    default: break;
+                }
             }
         }
         size_t blocks = (n + kThreads - 1) / kThreads;

@@ -155,6 +155,26 @@ __device__ __forceinline__ T ring_elem(const SmallRingArgs &a, int c, size_t i)
     return fold_elem<T, OP, NP, SOSX_ORDER_LINEAR>(v);
 }
 
+// The same, team size at run time, one element per lane (operands not 16-B aligned).
+template <class T, class OP>
+__global__ __launch_bounds__(kThreads) void k_small_ring_dyn(T *out, SmallRingArgs a, int np)
+{
+    const uint64_t b = blockIdx.x;
+    int c = 0;
+    while (b >= a.tstart[c + 1]) ++c;
+    const uint64_t j = (b - a.tstart[c]) * kThreads + threadIdx.x;
+    if (j < a.nvec[c]) {
+        const size_t i = a.first[c] + j;
+        T acc = ((const T *)a.in[c])[i];
+        for (int k = 1; k < np; ++k) {
+            const int pe = c + k < np ? c + k : c + k - np;
+            acc = OP::f(acc, ((const T *)a.in[pe])[i]);
+        }
+        out[i] = acc;
+    }
+    signal_done(a.flags, a.seq);
+}
+
 template <class T, class OP, int NP, bool VEC>
 __global__ __launch_bounds__(kThreads) void k_small_ring(T *out, SmallRingArgs a)
 {
@@ -260,8 +280,8 @@ struct SmallFoldFn {
         if (vec)                                                                                   \
             hipLaunchKernelGGL((k_small_fold<T, OP, P2, true, SmallFoldArgs8>), dim3(blocks),       \
                                dim3(kThreads), 0, st, (T *)out, a8, n);                            \
-        else                                                                                       \
-            hipLaunchKernelGGL((k_small_fold<T, OP, P2, false, SmallFoldArgs8>), dim3(blocks),      \
+        else  /* unaligned operands: one element per lane, leaf count at run time */             \
+            hipLaunchKernelGGL((k_small_fold<T, OP, 0, false, SmallFoldArgs8>), dim3(blocks),       \
                                dim3(kThreads), 0, st, (T *)out, a8, n);                            \
         break;
             SOS_SMALL(1)
@@ -281,15 +301,16 @@ struct SmallRingFn {
     template <class T, class OP>
     static int run(void *out, const SmallRingArgs *a, int np, bool vec, unsigned blocks, hipStream_t st)
     {
+        if (!vec) {  // unaligned operands: one element per lane, team size at run time
+            if (np < 1 || np > 8) return SOSX_ERR_ARG;
+            hipLaunchKernelGGL((k_small_ring_dyn<T, OP>), dim3(blocks), dim3(kThreads), 0, st, (T *)out, *a, np);
+            return hip_ok(hipGetLastError());
+        }
         switch (np) {
 #define SOS_RING(NP)                                                                               \
     case NP:                                                                                       \
-        if (vec)                                                                                   \
-            hipLaunchKernelGGL((k_small_ring<T, OP, NP, true>), dim3(blocks), dim3(kThreads), 0, st, \
-                               (T *)out, *a);                                                      \
-        else                                                                                       \
-            hipLaunchKernelGGL((k_small_ring<T, OP, NP, false>), dim3(blocks), dim3(kThreads), 0, st, \
-                               (T *)out, *a);                                                      \
+        hipLaunchKernelGGL((k_small_ring<T, OP, NP, true>), dim3(blocks), dim3(kThreads), 0, st,     \
+                           (T *)out, *a);                                                          \
         break;
             SOS_RING(1)
             SOS_RING(2)

@@ -394,237 +394,3 @@ int sosxv_prefix(int v, void *const *outs, const void *const *ins, int np, size_
 }
 
 }  // extern "C"
-
-// ---------------------------------------------------------------------------------
-// Host-side completion latency probe (bench only): the cost of learning that one tiny
-// kernel finished, by the ways a library call can wait.  mode 0: hipStreamSynchronize;
-// 1: spin on hipStreamQuery; 2: hipEventRecord + hipEventSynchronize; 3: the kernel
-// stores a flag into pinned host memory (system scope) and the host spins on it; 4: as
-// 3 after one hipStreamQuery of the busy stream; 5: one hipStreamQuery of an idle
-// stream alone (no launch); 6: as 3 with a RELAXED system-scope store (no release fence,
-// so no L2 write-back before it); 7: as 3 from a 1024-thread workgroup (the small path's
-// copy kernel shape).  Modes 3, 4, 6, 7 use a coherent (fine-grained) flag, as the
-// product's completion words.
-// Returns the mean microseconds per launch+wait over `iters`.
-// ---------------------------------------------------------------------------------
-__global__ void k_probe_flag(unsigned *flag, unsigned v)
-{
-    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__global__ void k_probe_flag_relaxed(unsigned *flag, unsigned v)
-{
-    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-#include <chrono>
-
-extern "C" double sosxv_sync_probe(int mode, int iters, void *stream)
-{
-    hipStream_t st = as_stream(stream);
-    unsigned *flag = nullptr;
-    if (hipHostMalloc((void **)&flag, 64, hipHostMallocCoherent) != hipSuccess) return -1.0;
-    *flag = 0;
-    hipEvent_t ev;
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1.0;
-    double total = 0;
-    for (int it = -10; it < iters; ++it) {
-        const auto t0 = std::chrono::steady_clock::now();
-        const unsigned v = (unsigned)(it + 11);
-        if (mode == 6)
-            hipLaunchKernelGGL(k_probe_flag_relaxed, dim3(1), dim3(64), 0, st, flag, v);
-        else
-            hipLaunchKernelGGL(k_probe_flag, dim3(1), dim3(mode == 7 ? 1024 : 64), 0, st, flag, v);
-        if (mode == 0) (void)hipStreamSynchronize(st);
-        else if (mode == 1) { while (hipStreamQuery(st) == hipErrorNotReady) {} }
-        else if (mode == 2) { (void)hipEventRecord(ev, st); (void)hipEventSynchronize(ev); }
-        else if (mode == 5) {  // one hipStreamQuery on an IDLE stream (no launch): its cost
-            (void)hipStreamSynchronize(st);
-            const auto q0 = std::chrono::steady_clock::now();
-            (void)hipStreamQuery(st);
-            const auto q1 = std::chrono::steady_clock::now();
-            if (it >= 0) total += std::chrono::duration<double, std::micro>(q1 - q0).count();
-            continue;
-        } else {  // bounded: a flag that never arrives returns an error after 2 s
-            if (mode == 4) (void)hipStreamQuery(st);  // one query of the busy stream first
-            while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != v) {
-                __builtin_ia32_pause();
-                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-                    (void)hipStreamSynchronize(st);
-                    (void)hipEventDestroy(ev);
-                    (void)hipHostFree(flag);
-                    return -2.0;
-                }
-            }
-        }
-        const auto t1 = std::chrono::steady_clock::now();
-        if (it >= 0) total += std::chrono::duration<double, std::micro>(t1 - t0).count();
-    }
-    (void)hipStreamSynchronize(st);
-    (void)hipEventDestroy(ev);
-    (void)hipHostFree(flag);
-    return total / iters;
-}
-
-// ---------------------------------------------------------------------------------
-// Host <-> GPU round trip through pinned memory with NO launch per request (bench only):
-// the lower bound of a persistent-service design for small host-resident reductions.
-// One workgroup polls a request word in pinned host memory; on request k it reads
-// `n` floats from each of two pinned slots, stores their sum into a pinned result and
-// then acknowledges k.  The host times write-request -> see-ack.  Exit conditions every
-// wave reaches: after `iters` requests, or when one wait exceeds `limit` wall-clock
-// ticks (the kernel then stores an error ack and returns); the host bounds its own
-// waits at 2 s and always synchronises the stream before returning.
-// ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_probe_service(const unsigned *req, unsigned *ack,
-                                                      const float *a, const float *b, float *out,
-                                                      int n, int iters, long long limit)
-{
-    for (int k = 1; k <= iters; ++k) {
-        if (threadIdx.x == 0) {
-            const long long t0 = wall_clock64();
-            while (__hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < (unsigned)k) {
-                if (wall_clock64() - t0 > limit) {
-                    __hip_atomic_store(ack, 0xFFFFFFFFu, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-                    k = iters + 1;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        __shared__ int stop;
-        if (threadIdx.x == 0) stop = k > iters;
-        __syncthreads();
-        if (stop) return;
-        for (int i = threadIdx.x; i < n; i += 256) {
-            const float x = __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            const float y = __hip_atomic_load(b + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(out + i, x + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(ack, (unsigned)k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-extern "C" double sosxv_service_probe(int n, int iters, void *stream)
-{
-    hipStream_t st = as_stream(stream);
-    if (n < 0 || n > 65536 || iters < 1) return -1.0;
-    unsigned *words = nullptr;
-    float *buf = nullptr;
-    if (hipHostMalloc((void **)&words, 256, hipHostMallocDefault) != hipSuccess) return -1.0;
-    if (hipHostMalloc((void **)&buf, 3 * 65536 * sizeof(float), hipHostMallocDefault) != hipSuccess) {
-        (void)hipHostFree(words);
-        return -1.0;
-    }
-    unsigned *req = words, *ack = words + 32;
-    *req = 0;
-    *ack = 0;
-    float *a = buf, *b = buf + 65536, *out = buf + 2 * 65536;
-    for (int i = 0; i < n; ++i) {
-        a[i] = (float)i;
-        b[i] = 0.5f;
-    }
-    int khz = 0;
-    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
-    const long long limit = (long long)(khz > 0 ? khz : 100000) * 2000;  // 2 s of ticks
-    const int total = iters + 10;
-    hipLaunchKernelGGL(k_probe_service, dim3(1), dim3(256), 0, st, req, ack, a, b, out, n, total, limit);
-    double sum = 0;
-    bool bad = hipGetLastError() != hipSuccess;
-    for (int k = 1; k <= total && !bad; ++k) {
-        const auto t0 = std::chrono::steady_clock::now();
-        __atomic_store_n(req, (unsigned)k, __ATOMIC_RELEASE);
-        unsigned v;
-        while ((v = __atomic_load_n(ack, __ATOMIC_ACQUIRE)) != (unsigned)k) {
-            __builtin_ia32_pause();
-            if (v == 0xFFFFFFFFu || std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-                bad = true;
-                break;
-            }
-        }
-        const auto t1 = std::chrono::steady_clock::now();
-        if (k > 10) sum += std::chrono::duration<double, std::micro>(t1 - t0).count();
-    }
-    if (bad) __atomic_store_n(req, 0xFFFFFFFEu, __ATOMIC_RELEASE);  // lets the kernel run out
-    (void)hipStreamSynchronize(st);
-    bool ok = !bad;
-    for (int i = 0; i < n && ok; ++i) ok = out[i] == (float)i + 0.5f;
-    (void)hipHostFree(buf);
-    (void)hipHostFree(words);
-    return ok ? sum / iters : -2.0;
-}
-
-// ---------------------------------------------------------------------------------
-// Kernel reads of host memory by allocation kind (bench only): what the small
-// host-resident path's slots should be.  mode 0: hipHostMalloc coherent; 1: hipHostMalloc
-// non-coherent; 2: mmap + hipHostRegister (fine grained, the small path today);
-// 3: mmap + hipHostRegister(hipExtHostRegisterCoarseGrained).  Every iteration the host
-// writes a new pattern, then ONE kernel reads the whole buffer (16 B per lane) and counts
-// words that do not carry the pattern (stale data after a host write); returns GB/s of
-// the kernel reads (host events around the launch + synchronisation, pattern write not
-// timed) and the stale-word count.
-// ---------------------------------------------------------------------------------
-#include <sys/mman.h>
-
-__global__ __launch_bounds__(256) void k_host_read(const u32x4 *p, size_t nvec, unsigned pat,
-                                                  unsigned long long *bad)
-{
-    unsigned long long b = 0;
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (size_t)gridDim.x * 256) {
-        const u32x4 v = p[i];
-        b += (v[0] != pat) + (v[1] != pat) + (v[2] != pat) + (v[3] != pat);
-    }
-    if (b) atomicAdd(bad, b);
-}
-
-extern "C" int sosxv_host_read_probe(int mode, size_t bytes, int iters, double *gbps,
-                                     unsigned long long *stale, void *stream)
-{
-    hipStream_t st = as_stream(stream);
-    void *buf = nullptr;
-    bool mapped = false;
-    if (mode == 0 || mode == 1) {
-        if (hipHostMalloc(&buf, bytes, mode == 0 ? hipHostMallocCoherent : hipHostMallocNonCoherent) != hipSuccess)
-            return -1;
-    } else {
-        buf = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
-        if (buf == MAP_FAILED) return -1;
-        mapped = true;
-        const unsigned fl = hipHostRegisterMapped | (mode == 3 ? hipExtHostRegisterCoarseGrained : 0);
-        if (hipHostRegister(buf, bytes, fl) != hipSuccess) {
-            munmap(buf, bytes);
-            return -2;
-        }
-    }
-    void *dptr = buf;
-    if (mapped && hipHostGetDevicePointer(&dptr, buf, 0) != hipSuccess) return -3;
-    unsigned long long *bad = nullptr;
-    if (hipMalloc((void **)&bad, 8) != hipSuccess) return -4;
-    (void)hipMemsetAsync(bad, 0, 8, st);
-    const size_t nvec = bytes / 16;
-    unsigned blocks = (unsigned)((nvec + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
-    double total = 0;
-    for (int it = -2; it < iters; ++it) {
-        const unsigned pat = 0x1000u + (unsigned)(it + 2);
-        unsigned *w = (unsigned *)buf;
-        for (size_t i = 0; i < bytes / 4; ++i) w[i] = pat;
-        __atomic_thread_fence(__ATOMIC_SEQ_CST);
-        const auto t0 = std::chrono::steady_clock::now();
-        hipLaunchKernelGGL(k_host_read, dim3(blocks), dim3(256), 0, st, (const u32x4 *)dptr, nvec, pat, bad);
-        (void)hipStreamSynchronize(st);
-        const auto t1 = std::chrono::steady_clock::now();
-        if (it >= 0) total += std::chrono::duration<double>(t1 - t0).count();
-    }
-    (void)hipMemcpy(stale, bad, 8, hipMemcpyDeviceToHost);
-    *gbps = (double)bytes * iters / total / 1e9;
-    (void)hipFree(bad);
-    if (mapped) {
-        (void)hipHostUnregister(buf);
-        munmap(buf, bytes);
-    } else {
-        (void)hipHostFree(buf);
-    }
-    return 0;
-}

@@ -58,33 +58,3 @@ def prefix(v, outs, ins, n, stream=None):
     o = (ctypes.c_void_p * k)(*outs)
     i = (ctypes.c_void_p * k)(*ins)
     _check(lib().sosxv_prefix(v, o, i, k, n, stream), "sosxv_prefix")
-
-
-def sync_probe(mode, iters=2000, stream=None):
-    """Mean us per tiny-kernel launch + completion wait (variants.hip sosxv_sync_probe)."""
-    L = lib()
-    L.sosxv_sync_probe.restype = ctypes.c_double
-    L.sosxv_sync_probe.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
-    return L.sosxv_sync_probe(mode, iters, stream)
-
-
-def service_probe(n, iters=2000, stream=None):
-    """Mean us per host->GPU->host round trip of a persistent one-workgroup kernel that
-    adds two n-float pinned slots per request (variants.hip sosxv_service_probe)."""
-    L = lib()
-    L.sosxv_service_probe.restype = ctypes.c_double
-    L.sosxv_service_probe.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
-    return L.sosxv_service_probe(n, iters, stream)
-
-
-def host_read_probe(mode, nbytes, iters=20, stream=None):
-    """(GB/s, stale words) of one kernel reading `nbytes` of host memory of kind `mode`
-    after the host rewrote it (variants.hip sosxv_host_read_probe)."""
-    L = lib()
-    L.sosxv_host_read_probe.restype = ctypes.c_int
-    L.sosxv_host_read_probe.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
-                                        ctypes.POINTER(ctypes.c_double),
-                                        ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_void_p]
-    g, s = ctypes.c_double(0), ctypes.c_ulonglong(0)
-    rc = L.sosxv_host_read_probe(mode, nbytes, iters, ctypes.byref(g), ctypes.byref(s), stream)
-    return (round(g.value, 2), int(s.value)) if rc == 0 else (rc, None)
