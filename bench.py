@@ -465,17 +465,39 @@ def cpu_baseline(args):
 
 
 CURVE_SIZES = (1 << 20, 4 << 20, 16 << 20, 64 << 20, 128 << 20, 256 << 20)
+MALL_BYTES = 256 << 20         # MI355X Infinity Cache (MALL), chip total
+ROTATE_BYTES = 1 << 30         # operand bytes a rotation cycles through per size point
+
+
+def time_launches(torch, stream, launches, reps):
+    """Mean HIP-event time per launch of `reps` back-to-back calls of launches[i % len]."""
+    for k in range(min(3, len(launches))):
+        launches[k]()
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s0.record(stream)
+    for r in range(reps):
+        launches[r % len(launches)]()
+    s1.record(stream)
+    torch.cuda.synchronize()
+    return s0.elapsed_time(s1) / 1e3 / reps
 
 
 def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
     """The north star's N = 1 curve: the device combine (sosx_combine) at nreduce =
-    1Mi .. 256Mi, each point with the mean HIP-event kernel time over a batch of
-    back-to-back launches, HBM GB/s (3 * n * s per launch) and its fraction of peak,
-    payload GiB/s, and beside it SOS's own CPU reduce_local (the oracle restatement of
+    1Mi .. 256Mi, and beside it SOS's own CPU reduce_local (the oracle restatement of
     src/shmem_internal_op.h:23-33,305-339, gcc -O2, 1 pinned thread) on the same inputs,
-    timed for about `cpu_seconds` per point.  Points <= 16Mi keep their three streams in
-    the 256 MiB Infinity Cache between launches, so they read above the HBM rate (and
-    the CPU's 1Mi point runs from its own caches)."""
+    timed for about `cpu_seconds` per point.
+
+    Two GPU timings per point, both the mean HIP-event kernel time over a batch of
+    back-to-back launches:
+      * HBM-streamed (`kernel_us`, `GBs`, `frac_hbm`): each launch takes the next of k
+        operand pairs, k * 2 * n * s >= 1 GiB, so a pair's bytes have left the 256 MiB
+        Infinity Cache before it comes round again -- every launch streams from HBM, and
+        `frac_hbm` is an HBM fraction;
+      * resident (`resident_kernel_us`, `resident_GBs`): the same pair every launch.  Where
+        the three streams fit the Infinity Cache (`cache_resident`: 3 * n * s <= 256 MiB)
+        this reads above the HBM rate and is not roofline evidence."""
     from sos_amd import _lib as L
     O = None
     if cpu:
@@ -486,30 +508,32 @@ def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
     stream = torch.cuda.current_stream()
     S = stream.cuda_stream
     sizes = [m for m in CURVE_SIZES if m <= args.sweep_max]
-    nmax = max(sizes)
-    a = torch.empty(nmax * es, dtype=torch.uint8, device="cuda")
-    b = torch.empty_like(a)
     rows = []
     for m in sizes:
-        L.fill(dt, dist, SEED, 0, a.data_ptr(), m, 0, S)
-        L.fill(dt, dist, SEED, 1, b.data_ptr(), m, 0, S)
-        launch = lambda: L.combine(op, dt, a.data_ptr(), b.data_ptr(), m, S)  # noqa: E731
-        for _ in range(3):
-            launch()
-        reps = max(10, min(200, int(4e9 // (3 * m * es))))
-        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        s0.record(stream)
-        for _ in range(reps):
-            launch()
-        s1.record(stream)
-        torch.cuda.synchronize()
-        kern = s0.elapsed_time(s1) / 1e3 / reps
-        algo = 3 * m * es
+        nb = m * es
+        npairs = max(1, -(-ROTATE_BYTES // (2 * nb)))
+        bufs = []
+        for _ in range(npairs):
+            a = torch.empty(nb, dtype=torch.uint8, device="cuda")
+            b = torch.empty_like(a)
+            L.fill(dt, dist, SEED, 0, a.data_ptr(), m, 0, S)
+            L.fill(dt, dist, SEED, 1, b.data_ptr(), m, 0, S)
+            bufs.append((a, b))
+        launches = [(lambda a=a, b=b: L.combine(op, dt, a.data_ptr(), b.data_ptr(), m, S))
+                    for a, b in bufs]
+        reps = max(10, min(400, int(4e9 // (3 * nb))), 2 * npairs)
+        kern = time_launches(torch, stream, launches, reps)
+        resident = time_launches(torch, stream, launches[:1], max(10, min(200, int(4e9 // (3 * nb)))))
+        del launches, bufs
+        algo = 3 * nb
         row = {"nreduce": m, "kernel_us": round(kern * 1e6, 2),
                "GBs": round(algo / kern / 1e9, 1),
                "frac_hbm": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4),
-               "gpu_GiBs": round(m * es / kern / GiB, 2)}
+               "gpu_GiBs": round(nb / kern / GiB, 2),
+               "operand_pairs_rotated": npairs,
+               "resident_kernel_us": round(resident * 1e6, 2),
+               "resident_GBs": round(algo / resident / 1e9, 1),
+               "cache_resident": algo <= MALL_BYTES}
         if O is not None:
             inout = O.fill(dt, dist, SEED, 0, m)
             inp = O.fill(dt, dist, SEED, 1, m)
@@ -522,10 +546,13 @@ def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
             del inout, inp
         rows.append(row)
         log(f"[curve] n={m:>10} {row['kernel_us']:10.2f} us {row['GBs']:8.1f} GB/s "
-            f"frac {row['frac_hbm']:.3f}  cpu {row.get('cpu_GiBs')} GiB/s")
-    del a, b
+            f"frac {row['frac_hbm']:.3f} ({npairs} pairs)  resident {row['resident_GBs']:8.1f} GB/s"
+            f"  cpu {row.get('cpu_GiBs')} GiB/s")
     return {"op": args.op, "type": args.dtype, "kernel": "sos::k_combine3",
-            "gpu": "mean HIP-event kernel time over a batch of back-to-back launches",
+            "gpu": ("mean HIP-event kernel time over a batch of back-to-back launches; kernel_us / "
+                    "GBs / frac_hbm with the launches rotating over operand pairs of >= 1 GiB in "
+                    "all (HBM-streamed), resident_* on one pair (cache_resident: the three "
+                    "streams fit the 256 MiB Infinity Cache, not an HBM figure)"),
             "cpu": (f"oracle/sos_oracle.c reduce_local (SOS's loop, gcc -O2), 1 thread, "
                     f"~{cpu_seconds:g} s per point, same inputs" if cpu else "skipped"),
             "rows": rows}

@@ -267,6 +267,9 @@ def test_bench_team_leg(np_):
     res = json.loads(lines[0])
     assert res["n_gpus"] == np_ and res["value"] > 0
     assert res["config"]["transport"] in ("p2p", "p2p_host")
+    # np_ ranks on this box's one GPU: the line says so (device map, not a fixed text)
+    assert res["config"]["gpus_used"] == 1 and res["config"]["parallelism"] == f"pe{np_}_on_1gpu"
+    assert f"{np_} PEs on 1 GPU (shared" in res["config"]["workload"], res["config"]
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0
     # both p2p signalling modes measured and checked in every leg
     assert list(res["transports"]) == ["p2p", "p2p_host"], res["transports"]

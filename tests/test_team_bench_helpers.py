@@ -172,3 +172,14 @@ def test_workload_names_what_ran():
     assert "ncclAllGather" in TB.workload_text("rccl_ag", "float", "sum", 8, 2)
     assert "host-signalled" in TB.workload_text("p2p_host", "float", "sum", 8, 2)
     assert "no valid measurement" in TB.workload_text(None, "float", "sum", 8, 2)
+
+
+def test_workload_names_the_device_map():
+    """config.workload / parallelism come from the distinct GPUs the ranks reported: the
+    8-GPU node's line says 1 PE per MI355X, a one-GPU rehearsal says the GPU is shared."""
+    one_per = TB.workload_text("rccl", "float", "sum", 8, 8, 8)
+    assert "8 PEs on 8 GPUs (1 per MI355X)" in one_per
+    shared = TB.workload_text("p2p", "float", "sum", 8, 8, 1)
+    assert "8 PEs on 1 GPU (shared" in shared and "1 per MI355X" not in shared
+    assert TB.parallelism_text(8, 8) == "pe8" and TB.parallelism_text(8, 1) == "pe8_on_1gpu"
+    assert "4 PEs on 2 GPUs (shared" in TB.workload_text("p2p", "float", "sum", 8, 4, 2)

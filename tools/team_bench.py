@@ -77,9 +77,33 @@ def select_primary(results):
     return min(clean, key=lambda k: results[k]["t_step"]), None
 
 
-def workload_text(tname, dtype, op, n, world):
-    """config.workload for what actually ran."""
-    head = f"shmem_{dtype}_{op}_reduce(SHMEM_TEAM_WORLD) nreduce={n} per PE, {world} PEs (1 per MI355X), "
+def placement_text(world, ngpus):
+    """How the PEs sat on GPUs, from the device map the ranks reported (distinct devices)."""
+    if ngpus == world:
+        return f"{world} PEs on {ngpus} GPUs (1 per MI355X)"
+    return f"{world} PEs on {ngpus} GPU{'s' if ngpus != 1 else ''} (shared: not a 1-PE-per-GPU figure)"
+
+
+def parallelism_text(world, ngpus):
+    return f"pe{world}" if ngpus == world else f"pe{world}_on_{ngpus}gpu"
+
+
+def device_ident(torch, local):
+    """A string naming this rank's physical GPU (UUID, else PCI location)."""
+    props = torch.cuda.get_device_properties(local)
+    u = getattr(props, "uuid", None)
+    if u is not None and str(u).strip("0-"):
+        return str(u)
+    loc = [getattr(props, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+    if any(v is not None for v in loc):
+        return ":".join(str(v) for v in loc)
+    return f"{os.uname().nodename}/{local}"
+
+
+def workload_text(tname, dtype, op, n, world, ngpus=None):
+    """config.workload for what actually ran (ngpus: distinct GPUs the PEs ran on)."""
+    ngpus = world if ngpus is None else ngpus
+    head = f"shmem_{dtype}_{op}_reduce(SHMEM_TEAM_WORLD) nreduce={n} per PE, {placement_text(world, ngpus)}, "
     data_path = {
         "rccl": "ncclSend/ncclRecv over xGMI + HIP fold kernel",
         "rccl_ag": "ncclSend/ncclRecv + ncclAllGather over xGMI + HIP fold kernel",
@@ -162,6 +186,9 @@ def main(args, torch, pmc=None):
     # the device is opened only now: during the preflight the child PE job is the only
     # process on each GPU (counting devices above does not initialise the runtime)
     torch.cuda.set_device(local)
+    idents = [None] * world
+    dist.all_gather_object(idents, device_ident(torch, local))
+    ngpus = len(set(idents))
     S.shmem_init()
     assert S.shmem_n_pes() == world and S.shmem_my_pe() == rank
     alg = L.ALGS[args.alg]
@@ -312,9 +339,9 @@ def main(args, torch, pmc=None):
         "vs_baseline": None,
         "dtype": {"float": "f32", "double": "f64"}.get(args.dtype, args.dtype),
         "data": "synthetic (splitmix64 counter hash per PE, SURVEY.md 8(d)), resident in HBM",
-        "config": {"workload": workload_text(primary, args.dtype, args.op, n, world),
+        "config": {"workload": workload_text(primary, args.dtype, args.op, n, world, ngpus),
                    "nreduce": n, "algorithm": name, "transport": primary,
-                   "parallelism": f"pe{world}"},
+                   "parallelism": parallelism_text(world, ngpus), "gpus_used": ngpus},
         "roofline": {"bound": "hbm", "kernel": "sos::k_fold (fused P-way combine)",
                      "achieved": round(fold_bytes / (fold_ms / 1e3) / 1e9, 1) if fold_ms > 0 else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
