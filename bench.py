@@ -88,18 +88,83 @@ def log(*a):
 # ----------------------------------------------------------------------------------
 # N = 1: the local combine
 # ----------------------------------------------------------------------------------
-def combine_setup(args, torch, S):
+class DevBuf:
+    """A device buffer: from the library's device symmetric heap (shmemx_malloc_device,
+    where an SOS program keeps device-resident symmetric data) or from torch's caching
+    allocator.  .ptr is the device address."""
+
+    def __init__(self, torch, nbytes, heap):
+        self.heap = heap
+        if heap:
+            from sos_amd import shmem as SH
+            self.ptr = SH.shmemx_malloc_device(nbytes)
+            self.t = None
+        else:
+            self.t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+            self.ptr = self.t.data_ptr()
+
+    def free(self):
+        if self.heap and self.ptr:
+            from sos_amd import shmem as SH
+            SH.lib().shmemx_free_device(self.ptr)
+        self.ptr, self.t = 0, None
+
+
+_SHMEM_UP = False
+
+
+def shmem_up(args):
+    """shmem_init() for the N = 1 legs (one PE): the device symmetric heap holds their
+    operands.  The heap is sized for the largest leg (the combine's two operands, or the
+    prefix's 2P chunks) plus its stage region."""
+    global _SHMEM_UP
+    if _SHMEM_UP:
+        return
+    from sos_amd import _lib as L
+    from sos_amd import shmem as SH
+    es = L.dtype_size(L.dtype_id(args.dtype))
+    os.environ.setdefault("SHMEMX_STAGE_BYTES", str(64 << 20))
+    big = max(2 * args.n * es, 2 * max(CURVE_SIZES) * es, ROTATE_BYTES)
+    os.environ.setdefault("SHMEMX_DEVICE_HEAP_SIZE", str(big + (512 << 20)))
+    SH.shmem_init()
+    _SHMEM_UP = True
+
+
+def combine_setup(args, torch, S, heap=True):
     from sos_amd import _lib as L
     dt = L.dtype_id(args.dtype)
     es = L.dtype_size(dt)
     nbytes = args.n * es
-    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    if heap:
+        shmem_up(args)
+    a, b = DevBuf(torch, nbytes, heap), DevBuf(torch, nbytes, heap)
     dist = L.DIST_PROD if args.op == "prod" else L.DIST_UNIFORM
-    L.fill(dt, dist, SEED, 0, a.data_ptr(), args.n, 0, S)
-    L.fill(dt, dist, SEED, 1, b.data_ptr(), args.n, 0, S)
+    L.fill(dt, dist, SEED, 0, a.ptr, args.n, 0, S)
+    L.fill(dt, dist, SEED, 1, b.ptr, args.n, 0, S)
     torch.cuda.synchronize()
     return L, dt, es, a, b
+
+
+def time_combine(args, torch, heap):
+    """The combine on a fresh operand pair, timed like the headline: (mean HIP-event ms
+    over K back-to-back launches, the pair's start-to-start distance in bytes)."""
+    stream = torch.cuda.current_stream()
+    S = stream.cuda_stream
+    L, dt, es, a, b = combine_setup(args, torch, S, heap)
+    op = L.op_id(args.op)
+    for _ in range(args.warmup):
+        L.combine(op, dt, a.ptr, b.ptr, args.n, S)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(args.steps):
+        L.combine(op, dt, a.ptr, b.ptr, args.n, S)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist_b = b.ptr - a.ptr
+    a.free()
+    b.free()
+    return e0.elapsed_time(e1) / args.steps, dist_b
 
 
 def run_combine(args, torch):
@@ -107,19 +172,21 @@ def run_combine(args, torch):
     S = stream.cuda_stream
     L, dt, es, a, b = combine_setup(args, torch, S)
     op = L.op_id(args.op)
-    launch = lambda: L.combine(op, dt, a.data_ptr(), b.data_ptr(), args.n, S)  # noqa: E731
+    launch = lambda: L.combine(op, dt, a.ptr, b.ptr, args.n, S)  # noqa: E731
 
     if args.child_pmc:  # profiled child: a few launches of each measured kernel only
         for _ in range(args.warmup + args.steps):
             launch()
         torch.cuda.synchronize()
-        del a, b
+        a.free()
+        b.free()
         for kind in ("fold", "prefix"):
             ms_launch, _, _, keep = multi_stream_setup(args, torch, kind)
             for _ in range(args.warmup + args.steps):
                 ms_launch()
             torch.cuda.synchronize()
-            del keep
+            for x in keep:
+                x.free()
         return None
 
     for _ in range(args.warmup):
@@ -150,6 +217,12 @@ def run_combine(args, torch):
         e_.record(stream)
     torch.cuda.synchronize()
     kern_ms = sorted(s_.elapsed_time(e_) for s_, e_ in ev)
+    dist_ab = b.ptr - a.ptr
+    a.free()
+    b.free()
+    # the same kernel on a pair from torch's caching allocator (2 MiB-aligned blocks), for
+    # comparison: the placement of a caller's own buffers is the caller's
+    torch_ms, torch_dist = time_combine(args, torch, heap=False)
     payload = args.n * es
     algo_bytes = 3 * payload  # read in, read inout, write inout
     achieved = algo_bytes / mean_kern_s / 1e9
@@ -177,6 +250,20 @@ def run_combine(args, torch):
                      "mean_kernel_ms_how": "HIP-event span of the timed region / steps",
                      "median_kernel_ms": round(kern_ms[len(kern_ms) // 2], 5),
                      "median_kernel_ms_how": "per-launch HIP event pairs, after the timed region"},
+        "operands": {"where": "device symmetric heap (shmemx_malloc_device), one PE",
+                     "in_minus_inout_bytes": dist_ab,
+                     "in_minus_inout_mod_32KiB": dist_ab % 32768,
+                     "note": "the heap starts large allocations an odd multiple of 4 KiB apart "
+                             "in HBM's 32 KiB channel interleave (DESIGN.md section 4, "
+                             "profiles/r4_offset_probe.txt)"},
+        "torch_allocator_buffers": {
+            "mean_kernel_ms": round(torch_ms, 5),
+            "achieved_GBs": round(algo_bytes / (torch_ms / 1e3) / 1e9, 1),
+            "frac": round(algo_bytes / (torch_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "in_minus_inout_bytes": torch_dist,
+            "in_minus_inout_mod_32KiB": torch_dist % 32768,
+            "note": "the same kernel and timing on two torch.empty buffers (the caller's "
+                    "placement, not the heap's): reported, never `value`"},
     }
     return res
 
@@ -243,18 +330,21 @@ def multi_stream_setup(args, torch, kind):
     chunk = args.n // P
     S = torch.cuda.current_stream().cuda_stream
     dist = L.DIST_PROD if args.op == "prod" else L.DIST_UNIFORM
-    ins = [torch.empty(chunk * es, dtype=torch.uint8, device="cuda") for _ in range(P)]
-    outs = [torch.empty_like(x) for x in ins[:P if kind == "prefix" else 1]]
+    shmem_up(args)
+    # heap buffers: consecutive large allocations are 4 KiB apart in the channel
+    # interleave, as the library's own scratch slots are (plan.cpp slot_stride)
+    ins = [DevBuf(torch, chunk * es, True) for _ in range(P)]
+    outs = [DevBuf(torch, chunk * es, True) for _ in range(P if kind == "prefix" else 1)]
     for k, x in enumerate(ins):
-        L.fill(dt, dist, SEED, k, x.data_ptr(), chunk, 0, S)
-    ip, op_ = [x.data_ptr() for x in ins], [x.data_ptr() for x in outs]
+        L.fill(dt, dist, SEED, k, x.ptr, chunk, 0, S)
+    ip, op_ = [x.ptr for x in ins], [x.ptr for x in outs]
     if kind == "prefix":
         launch = lambda: L.prefix("sum", dt, op_, ip, chunk, -1, S)  # noqa: E731
         algo = 2 * P * chunk * es
     else:
         launch = lambda: L.fold(args.op, dt, L.ORDER_LINEAR, op_[0], ip, chunk, S)  # noqa: E731
         algo = (P + 1) * chunk * es
-    return launch, algo, chunk, (ins, outs)
+    return launch, algo, chunk, ins + outs
 
 
 def multi_stream_kernel(args, torch, kind):
@@ -275,7 +365,8 @@ def multi_stream_kernel(args, torch, kind):
     s1.record(stream)
     torch.cuda.synchronize()
     mean_s = s0.elapsed_time(s1) / reps / 1e3
-    del keep
+    for x in keep:
+        x.free()
     P = args.fold_p
     name = {"prefix": f"sos::k_prefix<NP={P}>", "fold": f"sos::k_fold<NP={P}, LINEAR>"}[kind]
     return {"kernel": name, "inputs": P, "elements_per_input": chunk,
@@ -485,7 +576,7 @@ def time_launches(torch, stream, launches, reps):
 
 def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
     """The north star's N = 1 curve: the device combine (sosx_combine) at nreduce =
-    1Mi .. 256Mi, and beside it SOS's own CPU reduce_local (the oracle restatement of
+    1Mi .. 256Mi on device-symmetric-heap operands, and beside it SOS's own CPU reduce_local (the oracle restatement of
     src/shmem_internal_op.h:23-33,305-339, gcc -O2, 1 pinned thread) on the same inputs,
     timed for about `cpu_seconds` per point.
 
@@ -508,23 +599,25 @@ def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
     stream = torch.cuda.current_stream()
     S = stream.cuda_stream
     sizes = [m for m in CURVE_SIZES if m <= args.sweep_max]
+    shmem_up(args)
     rows = []
     for m in sizes:
         nb = m * es
         npairs = max(1, -(-ROTATE_BYTES // (2 * nb)))
         bufs = []
-        for _ in range(npairs):
-            a = torch.empty(nb, dtype=torch.uint8, device="cuda")
-            b = torch.empty_like(a)
-            L.fill(dt, dist, SEED, 0, a.data_ptr(), m, 0, S)
-            L.fill(dt, dist, SEED, 1, b.data_ptr(), m, 0, S)
+        for _ in range(npairs):  # device symmetric heap, as the headline's operands
+            a, b = DevBuf(torch, nb, True), DevBuf(torch, nb, True)
+            L.fill(dt, dist, SEED, 0, a.ptr, m, 0, S)
+            L.fill(dt, dist, SEED, 1, b.ptr, m, 0, S)
             bufs.append((a, b))
-        launches = [(lambda a=a, b=b: L.combine(op, dt, a.data_ptr(), b.data_ptr(), m, S))
-                    for a, b in bufs]
+        launches = [(lambda a=a, b=b: L.combine(op, dt, a.ptr, b.ptr, m, S)) for a, b in bufs]
         reps = max(10, min(400, int(4e9 // (3 * nb))), 2 * npairs)
         kern = time_launches(torch, stream, launches, reps)
         resident = time_launches(torch, stream, launches[:1], max(10, min(200, int(4e9 // (3 * nb)))))
-        del launches, bufs
+        del launches
+        for a, b in bufs:
+            a.free()
+            b.free()
         algo = 3 * nb
         row = {"nreduce": m, "kernel_us": round(kern * 1e6, 2),
                "GBs": round(algo / kern / 1e9, 1),
@@ -603,6 +696,9 @@ def main():
     if rank == 0 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(res), flush=True)
+    if _SHMEM_UP:
+        from sos_amd import shmem as SH
+        SH.shmem_finalize()
     return 0
 
 

@@ -38,6 +38,18 @@ Local fold2(int out_buf, uint64_t out_off, int a_buf, uint64_t a_off, int b_buf,
     return l;
 }
 
+// Stride between the scratch slots a fold or prefix reads together.  Large slots: a
+// multiple of 32 KiB plus 4 KiB, so slot k starts k * 4 KiB into HBM's 32 KiB channel
+// interleave and the P-1 slots walk different channels (tools/offset_probe.py --multi,
+// profiles/r4_offset_probe.txt: the 8-input fold over 4 KiB-staggered streams 6.13-6.18
+// TB/s, over streams 0 mod 32 KiB apart 5.80-5.91; the 16-stream prefix 5.95 vs 5.68-5.72).
+// Small slots keep the 1 KiB step (the fold over them is latency-bound).
+static uint64_t slot_stride(uint64_t bytes)
+{
+    if (bytes < ((uint64_t)1 << 20)) return round_up(bytes + 16, 1024);
+    return round_up(bytes + 16, 32768) + 4096;
+}
+
 // RING and RECDBL_DIRECT share the data movement: a direct reduce-scatter of the SOS
 // ring chunks (chunk c is owned, folded and broadcast by team index c), then a
 // direct allgather.  Only the fold order differs.
@@ -48,14 +60,12 @@ int build_direct(int alg, int P, int me, uint64_t count, uint64_t ts, unsigned s
     uint64_t n_me, first_me;
     ring_chunk(count, P, me, &n_me, &first_me);
     const uint64_t my_bytes = n_me * ts;
-    // Scratch slot for each peer's copy of my chunk, 16-B congruent with my DST chunk.
-    // Consecutive slots sit chunk + 1 KiB apart (for 1 KiB-multiple chunks): the P-input
-    // fold over them streams ~2 % faster than with 256-B skews (tools/fold_layout_probe.py
-    // on two boxes, profiles/r3_fold_layout_probe.json: 5.96-5.98 vs 5.83-5.84 TB/s); in
-    // the 8-PE loopback ring the fold's mean moved 102.3 -> 101.7 us, inside its 94-110 us
-    // per-PE spread (the caller's own source and target placement dominates there).
+    // Scratch slot for each peer's copy of my chunk, 16-B congruent with my DST chunk,
+    // slot_stride apart (round 3: chunk + 1 KiB, ~2 % faster than 256-B skews,
+    // profiles/r3_fold_layout_probe.json; round 4: 4 KiB steps in the channel interleave
+    // for chunks of 1 MiB and more).
     const uint64_t mis = (dst_mis + first_me * ts) & 15;
-    const uint64_t stride = round_up(my_bytes + 16, 1024);
+    const uint64_t stride = slot_stride(my_bytes);
     auto slot = [&](int peer) { return (uint64_t)((peer - me - 1 + P) % P) * stride + mis; };
     (void)src_mis;
     plan->scratch_bytes = (uint64_t)(P - 1) * stride;
@@ -289,7 +299,7 @@ int build_scan(bool exclusive, int P, int me, uint64_t count, uint64_t ts, unsig
     ring_chunk(count, P, me, &n_me, &first_me);
     const uint64_t my_bytes = n_me * ts;
     const uint64_t mis = (dst_mis + first_me * ts) & 15;
-    const uint64_t stride = round_up(my_bytes + 16, 256);
+    const uint64_t stride = my_bytes < ((uint64_t)1 << 20) ? round_up(my_bytes + 16, 256) : slot_stride(my_bytes);
     (void)src_mis;
     // SCR: P-1 slots for the peers' copies of my chunk, then P-1 slots for my chunk of
     // the peers' results

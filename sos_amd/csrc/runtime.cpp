@@ -274,7 +274,19 @@ void Heap::init(char *b, size_t s, bool dev, bool ext)
     free_blocks.clear();
     used_blocks.clear();
     free_blocks[0] = s;
+    colour_seq = 0;
 }
+
+// Colours of large device-heap allocations.  The HBM rate of a streaming kernel depends on
+// how far apart its operands start (tools/offset_probe.py, profiles/r4_offset_probe.txt,
+// 128Mi fp32 combine, in = inout + 512 MiB + delta): delta a multiple of 32 KiB below
+// 1 MiB, or a multiple of 16 MiB, runs at 6.22-6.32 TB/s (the two read streams walk the
+// same HBM channels in step); every odd multiple of 4 KiB probed runs at 6.55-6.67.  So
+// the k-th allocation of at least kColorMin bytes starts at (k mod 8) * 4 KiB mod 32 KiB
+// from the heap base: consecutive large buffers (a source and its target, a fold's
+// inputs) are an odd multiple of 4 KiB apart.  The colour depends only on the allocation
+// sequence, which SOS makes collective, so offsets stay symmetric across PEs.
+constexpr size_t kColorMin = (size_t)1 << 20, kColorStep = 4096, kColorPeriod = 32768;
 
 void *Heap::alloc(size_t bytes, size_t align)
 {
@@ -282,14 +294,18 @@ void *Heap::alloc(size_t bytes, size_t align)
     if (align < 256) align = 256;
     if (bytes == 0) bytes = 1;
     bytes = (bytes + 255) & ~(size_t)255;
+    const bool colour = device && bytes >= kColorMin && align <= kColorStep;
+    const size_t want = colour ? (size_t)(colour_seq % (kColorPeriod / kColorStep)) * kColorStep : 0;
     for (auto it = free_blocks.begin(); it != free_blocks.end(); ++it) {
         size_t off = it->first, len = it->second;
         size_t aoff = (off + align - 1) / align * align;
+        if (colour) aoff += (want + kColorPeriod - aoff % kColorPeriod) % kColorPeriod;
         if (aoff + bytes > off + len) continue;
         free_blocks.erase(it);
         if (aoff > off) free_blocks[off] = aoff - off;
         if (off + len > aoff + bytes) free_blocks[aoff + bytes] = off + len - (aoff + bytes);
         used_blocks[aoff] = bytes;
+        if (colour) ++colour_seq;
         return base + aoff;
     }
     return nullptr;
@@ -651,7 +667,8 @@ void shmem_init(void)
         blob.transport = s.transport;
         blob.want_rccl = s.want_rccl;
         blob.want_p2p = s.want_p2p;
-        if (blob.want_rccl) nccl_check(ncclGetUniqueId(&blob.uid), "ncclGetUniqueId");
+        // one PE has no peers: no communicator (RCCL's init also prints a banner to stdout)
+        if (blob.want_rccl && size > 1) nccl_check(ncclGetUniqueId(&blob.uid), "ncclGetUniqueId");
         snprintf(blob.shm_name, sizeof(blob.shm_name), "/sosx_%d_%lx", (int)getpid(),
                  (unsigned long)time(nullptr));
     }
@@ -682,7 +699,7 @@ void shmem_init(void)
         sosboot::hub_allgather(&s.hub, &dummy, sizeof(dummy), all.data());
         if (rank == 0) shm_unlink(blob.shm_name);
     }
-    init_common(rank, size, s.want_rccl ? &blob.uid : nullptr);
+    init_common(rank, size, s.want_rccl && size > 1 ? &blob.uid : nullptr);
 }
 
 int shmem_init_thread(int requested, int *provided)
@@ -957,7 +974,7 @@ int shmemx_set_transport(int transport)
 {
     State &s = st();
     const int prev = s.transport;
-    if (transport == TRANSPORT_RCCL && s.comm) s.transport = TRANSPORT_RCCL;
+    if (transport == TRANSPORT_RCCL && (s.comm || s.n_pes == 1)) s.transport = TRANSPORT_RCCL;
     else if (transport == TRANSPORT_P2P && s.p2p_ready && (s.shm.base || s.n_pes == 1))
         s.transport = TRANSPORT_P2P;
     else return -1;

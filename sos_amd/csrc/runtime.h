@@ -55,6 +55,7 @@ struct Heap {
     bool external = false;
     std::map<size_t, size_t> free_blocks;  // offset -> size
     std::map<size_t, size_t> used_blocks;  // offset -> size
+    uint64_t colour_seq = 0;               // large device allocations so far (Heap::alloc)
     void init(char *b, size_t s, bool dev, bool ext);
     void *alloc(size_t bytes, size_t align);
     bool release(void *p);

@@ -35,5 +35,9 @@ def test_bench_n1_line():
         assert row["operand_pairs_rotated"] * 2 * row["nreduce"] * 4 >= 1 << 30, row
         assert row["cache_resident"] == (3 * row["nreduce"] * 4 <= 256 << 20), row
         assert row["cpu_GiBs"] > 0
+    # operands from the device symmetric heap, started an odd multiple of 4 KiB apart in
+    # the 32 KiB channel interleave; the torch-allocator pair is reported beside it
+    assert res["operands"]["in_minus_inout_mod_32KiB"] % 8192 == 4096, res["operands"]
+    assert 0 < res["torch_allocator_buffers"]["frac"] <= 1
     cpu = res["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["cores"] == 1 and cpu["value"] > 0

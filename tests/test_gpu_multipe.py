@@ -204,6 +204,19 @@ def test_route_mismatch_ends_the_job_at_once():
     assert t_end - max(starts) < 10, t_end - max(starts)  # teardown included; 60 s if missed
 
 
+def test_device_heap_colours():
+    """Large device-heap allocations step through the 32 KiB channel interleave in 4 KiB
+    colours (consecutive ones an odd multiple of 4 KiB apart), at the same offsets on
+    every PE (symmetric)."""
+    r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "heap_colour_pe.py")], timeout=120,
+               extra_env={"SHMEMX_DEVICE_HEAP_SIZE": "1G"})
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    # PEs print concurrently: match the reports, not lines
+    lines = re.findall(r"PE \d: (colours \[[\d, ]+\] offsets \[[\d, ]+\])", r.stdout)
+    assert len(lines) == 2 and lines[0] == lines[1], r.stdout
+    assert "colours [0, 1, 2, 3, 4, 5, 6, 7, 0, 1]" in lines[0], lines
+
+
 def test_small_device_setter_is_collective():
     """sosx_set_small_device_bytes with different limits on two PEs is refused."""
     r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "route_mismatch_pe.py"), "setter"],

@@ -1,0 +1,122 @@
+"""Bench-only probe: does the 128Mi fp32 combine's HBM rate depend on where its operands
+sit relative to each other (DRAM channel / bank aliasing of the two read streams and the
+write stream)?  One big allocation; inout at offset A, in at offset B = A + 512 MiB +
+delta; the mean HIP-event time of back-to-back sosx_combine launches per delta.
+
+Usage: python tools/offset_probe.py [--n 134217728] [--reps 20]
+Prints one JSON line: {delta_bytes: GB/s}.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=128 << 20)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--fine", action="store_true",
+                    help="delta = k * 4 KiB (k < 64) and m * 1 MiB (m < 40), two base offsets")
+    args = ap.parse_args()
+    import torch
+    from sos_amd import _lib as L
+    torch.cuda.set_device(0)
+    n, es = args.n, 4
+    nb = n * es
+    span = 2 * nb + (128 << 20)
+    big = torch.empty(span, dtype=torch.uint8, device="cuda")
+    base = (big.data_ptr() + (2 << 20) - 1) & ~((2 << 20) - 1)  # 2 MiB aligned
+    S = torch.cuda.current_stream()
+    deltas = [0, 256, 1024, 4096, 8192, 16384, 32768, 65536, 128 << 10, 256 << 10, 512 << 10,
+              1 << 20, 3 << 20, 5 << 20, 7 << 20, 11 << 20, 13 << 20, 17 << 20, 23 << 20, 31 << 20]
+    bases = [0]
+    if args.fine:
+        deltas = [k * 4096 for k in range(64)] + [m << 20 for m in range(1, 40)]
+        bases = [0, 12288]
+    out = {}
+    for rnd in range(len(bases) if args.fine else 2):
+        for d in deltas:
+            a = base + bases[rnd % len(bases)]
+            b = base + nb + d
+            if b + nb > big.data_ptr() + span:
+                continue
+            L.fill(23, 0, 0x5EED, 0, a, n, 0, S.cuda_stream)
+            L.fill(23, 0, 0x5EED, 1, b, n, 0, S.cuda_stream)
+            for _ in range(3):
+                L.combine(5, 23, a, b, n, S.cuda_stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(S)
+            for _ in range(args.reps):
+                L.combine(5, 23, a, b, n, S.cuda_stream)
+            e1.record(S)
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1) / 1e3 / args.reps
+            gbs = 3 * nb / t / 1e9
+            out.setdefault(str(d), []).append(round(gbs, 1))
+            print(f"round {rnd} delta {d:>10}: {t * 1e3:.4f} ms {gbs:8.1f} GB/s", file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
+
+def multi(args):
+    """Fold (P inputs + 1 output) and prefix (P inputs + P outputs) with every stream in
+    one allocation, stream k at k * (chunk bytes + pad) + stagger(k); staggers: none
+    (all streams 0 mod 32 KiB apart), k * 4 KiB, k * 12 KiB, k * 4 KiB + 64 KiB * k."""
+    import torch
+    from sos_amd import _lib as L
+    torch.cuda.set_device(0)
+    P, chunk = 8, 16 << 20
+    nb = chunk * 4
+    nstreams = 2 * P
+    slot = nb + (1 << 20)
+    big = torch.empty(nstreams * slot + (4 << 20), dtype=torch.uint8, device="cuda")
+    base = (big.data_ptr() + (2 << 20) - 1) & ~((2 << 20) - 1)
+    S = torch.cuda.current_stream()
+    st = S.cuda_stream
+    schemes = {"aligned": lambda k: 0, "4k": lambda k: 4096 * k, "12k": lambda k: 12288 * k,
+               "4k_mod32k_odd": lambda k: 4096 * ((2 * k + 1) % 8), "36k": lambda k: 36864 * k}
+    out = {}
+    for rnd in range(2):
+        for name, f in schemes.items():
+            ptr = [base + k * slot + f(k) for k in range(nstreams)]
+            for k in range(P):
+                L.fill(23, 0, 0x5EED, k, ptr[k], chunk, 0, st)
+            for kind in ("fold", "prefix"):
+                if kind == "fold":
+                    launch = lambda: L.fold(5, 23, 0, ptr[P], ptr[:P], chunk, st)  # noqa: E731
+                    algo = (P + 1) * nb
+                else:
+                    launch = lambda: L.prefix(5, 23, ptr[P:2 * P], ptr[:P], chunk, -1, st)  # noqa: E731
+                    algo = 2 * P * nb
+                for _ in range(3):
+                    launch()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record(S)
+                for _ in range(args.reps):
+                    launch()
+                e1.record(S)
+                torch.cuda.synchronize()
+                t = e0.elapsed_time(e1) / 1e3 / args.reps
+                gbs = algo / t / 1e9
+                out.setdefault(f"{kind}/{name}", []).append(round(gbs, 1))
+                print(f"round {rnd} {kind:>6} {name:>14}: {t * 1e3:.4f} ms {gbs:8.1f} GB/s", file=sys.stderr,
+                      flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__" and "--multi" in sys.argv:
+    sys.argv.remove("--multi")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    multi(ap.parse_args())
+    sys.exit(0)
+
+
+if __name__ == "__main__":
+    main()
