@@ -121,7 +121,7 @@ def main():
                     mm = L.count_mismatch(exp.data_ptr(), out, n, es)
                     checks += 1
                     if mm:
-                        bad.append((alg, tname, oname, n, mode, mm))
+                        bad.append((alg, tname, oname, n, mode, mm, _where(exp, out, n, es)))
                 # split team: even PEs reduce among themselves
                 if even.value and n <= 5003:
                     L.fill(dt, dist, seed, me, hsrc, n)
@@ -228,6 +228,25 @@ def _perspective(a, pe):
     if a.size > 1:
         a.view(ity)[1] = (ity(0x7FC00000) if ity is np.uint32 else ity(0x7FF8000000000000)) | ity(pe + 1)
     return a
+
+
+def _where(exp, out, n, es):
+    """Diagnostics of a mismatch: the differing elements as [first, last) runs (at most 4),
+    and the count of a second comparison of the same bytes after a device synchronisation
+    (a different count means the target changed after the call returned)."""
+    torch.cuda.synchronize()
+    again = L.count_mismatch(exp.data_ptr(), out, n, es)
+    got = _download(out, n * es).reshape(n, es)
+    want = exp.cpu().numpy().reshape(n, es)
+    diff = np.nonzero((got != want).any(axis=1))[0]
+    runs = []
+    if diff.size:
+        cuts = np.nonzero(np.diff(diff) != 1)[0]
+        starts = np.concatenate(([diff[0]], diff[cuts + 1]))
+        ends = np.concatenate((diff[cuts], [diff[-1]])) + 1
+        runs = [(int(a), int(b)) for a, b in zip(starts[:4], ends[:4])]
+        runs.append(f"{starts.size} runs")
+    return {"recount": int(again), "runs": runs}
 
 
 def _download(ptr, nbytes):

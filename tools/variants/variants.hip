@@ -260,8 +260,71 @@ int fold_st(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 const char *const kFoldNames[] = {"u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd"};
 constexpr int kNumFold = 8;
 
-const char *const kPrefixNames[] = {"u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain", "u8_nt"};
-constexpr int kNumPrefix = 6;
+const char *const kPrefixNames[] = {"u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain", "u8_nt",
+                                    "split2_nt", "split2_seed_plain"};
+constexpr int kNumPrefix = 8;
+
+// Continuation of a prefix from a seed vector: out[k] = seed OP in[0] OP ... OP in[k],
+// left to right, so the second half of a split prefix is bit-identical to the fused one
+// (the running value is always the left operand, as in SOS scan_ring,
+// src/collectives.c:1188-1196).  The seed is read once and not stored.
+template <class T, class OP, int NP, bool NT, bool SEED_NT>
+__global__ __launch_bounds__(kThreads) void k_prefix_seeded(const T *seed, PrefixPtrs p, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        u32x4 acc = ldv<SEED_NT>(reinterpret_cast<const u32x4 *>(seed + g.head) + i);
+        u32x4 x[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            x[k] = ldv<NT>(reinterpret_cast<const u32x4 *>((const T *)p.in[k] + g.head) + i);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            acc = apply<T, OP>(acc, x[k]);
+            stv<NT>(reinterpret_cast<u32x4 *>((T *)p.out[k] + g.head) + i, acc);
+        }
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T acc = seed[i];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                acc = OP::f(acc, ((const T *)p.in[k])[i]);
+                ((T *)p.out[k])[i] = acc;
+            }
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
+// Split prefix: a fused prefix over the first H = NP/2 inputs, then a seeded prefix over
+// the rest, continuing from out[H-1].  Two 2H- and (2(NP-H)+1)-stream passes instead of one
+// 2NP-stream pass: 1/(2NP) more bytes, fewer concurrent DRAM streams per kernel.
+template <int NP, bool SEED_NT>
+int prefix_split2(const PrefixPtrs &p, size_t n, hipStream_t st)
+{
+    constexpr int H = NP / 2;
+    PrefixPtrs a, b;
+    memset(&a, 0, sizeof(a));
+    memset(&b, 0, sizeof(b));
+    for (int k = 0; k < H; ++k) {
+        a.in[k] = p.in[k];
+        a.out[k] = p.out[k];
+    }
+    for (int k = H; k < NP; ++k) {
+        b.in[k - H] = p.in[k];
+        b.out[k - H] = p.out[k];
+    }
+    Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), 1);
+    hipLaunchKernelGGL((k_prefix<T, OP, H, 1, true>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0,
+                       st, a, g);
+    hipLaunchKernelGGL((k_prefix_seeded<T, OP, NP - H, true, SEED_NT>), dim3(grid_for(g, kNoCap)),
+                       dim3(kThreads), 0, st, (const T *)p.out[H - 1], b, g);
+    return hip_ok(hipGetLastError());
+}
 
 template <int NP, int U, bool NT>
 int prefix_u(const PrefixPtrs &p, size_t n, hipStream_t st)
@@ -282,6 +345,8 @@ int prefix_np(int v, const PrefixPtrs &p, size_t n, hipStream_t st)
         case 3: return prefix_u<NP, 1, false>(p, n, st);
         case 4: return prefix_u<NP, 2, false>(p, n, st);
         case 5: return prefix_u<NP, 8, true>(p, n, st);
+        case 6: return prefix_split2<NP, true>(p, n, st);
+        case 7: return prefix_split2<NP, false>(p, n, st);
     }
     return SOSX_ERR_ARG;
 }
