@@ -21,6 +21,8 @@ def test_bench_n1_line():
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
+    # the driver reads stdout: the JSON line and nothing else
+    assert [ln for ln in r.stdout.splitlines() if ln.strip()] == lines, r.stdout[:2000]
     res = json.loads(lines[0])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):

@@ -276,6 +276,9 @@ def test_bench_team_leg(np_):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
+    # the driver reads stdout: rank 0's JSON line and nothing else (gloo's connection
+    # lines and any RCCL banner go to stderr)
+    assert [ln for ln in r.stdout.splitlines() if ln.strip()] == lines, r.stdout[:2000]
     import json
     res = json.loads(lines[0])
     assert res["n_gpus"] == np_ and res["value"] > 0

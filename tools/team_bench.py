@@ -155,6 +155,12 @@ def main(args, torch, pmc=None):
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank)) % max(torch.cuda.device_count(), 1)
+    # stdout carries rank 0's ONE JSON line and nothing else: what the native layers print
+    # there (gloo's "[Gloo] Rank i is connected to ..." lines, an RCCL banner) goes to
+    # stderr, and the line is written to the saved descriptor
+    sys.stdout.flush()
+    line_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     dt = L.dtype_id(args.dtype)
     es = L.dtype_size(dt)
     n = args.n
@@ -387,7 +393,8 @@ def main(args, torch, pmc=None):
     if small:
         res["small_messages"] = small
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        line_out.write(json.dumps(res) + "\n")
+        line_out.flush()
     dist.barrier()
     S.shmemx_free_device(dst)
     S.shmemx_free_device(src)
