@@ -254,7 +254,7 @@ def run_combine(args, torch):
                      "in_minus_inout_bytes": dist_ab,
                      "in_minus_inout_mod_32KiB": dist_ab % 32768,
                      "note": "the heap starts large allocations an odd multiple of 4 KiB apart "
-                             "in HBM's 32 KiB channel interleave (DESIGN.md section 4, "
+                             "in HBM's 32 KiB channel interleave (DESIGN.md section 3, "
                              "profiles/r4_offset_probe.txt)"},
         "torch_allocator_buffers": {
             "mean_kernel_ms": round(torch_ms, 5),
