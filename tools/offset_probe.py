@@ -110,6 +110,67 @@ def multi(args):
     print(json.dumps(out))
 
 
+def layouts(args):
+    """Fold (8 inputs + 1 output) and prefix (8 + 8) over 16 Mi-element fp32 streams
+    placed at base + k * spacing + colour(k) in one allocation: which spacings between
+    whole streams (above the 32 KiB channel interleave: DRAM bank / row bits) and which
+    4 KiB colours give the multi-stream kernels their best rate.  `order` io puts the
+    streams in memory as in0..in7, out0..out7; `rand` draws a random 4 KiB-page offset per
+    stream (0..63 pages, as tools/loopback_bench.py --prefix-ab does)."""
+    import random
+    import torch
+    from sos_amd import _lib as L
+    torch.cuda.set_device(0)
+    P, chunk = 8, 16 << 20
+    nb = chunk * 4
+    M, K = 1 << 20, 4096
+    spacings = {"64M": nb, "64M+64K": nb + 64 * 1024, "64M+256K": nb + 256 * 1024, "64M+1M": nb + M,
+                "64M+2M": nb + 2 * M, "64M+3M": nb + 3 * M, "66M": nb + 2 * M + 256 * 1024}
+    rng = random.Random(7)
+    colours = {"c0": lambda k: 0, "c4k": lambda k: K * (k % 8), "crand": lambda k: K * rng.randrange(64)}
+    big = torch.empty(2 * P * (nb + 4 * M) + 8 * M, dtype=torch.uint8, device="cuda")
+    base = (big.data_ptr() + (2 << 20) - 1) & ~((2 << 20) - 1)
+    S = torch.cuda.current_stream()
+    st = S.cuda_stream
+    out = {}
+    for rnd in range(2):
+        for sname, sp in spacings.items():
+            for cname, cf in colours.items():
+                ptr = [base + k * sp + cf(k) for k in range(2 * P)]
+                for k in range(P):
+                    L.fill(23, 0, 0x5EED, k, ptr[k], chunk, 0, st)
+                for kind in ("fold", "prefix"):
+                    if kind == "fold":
+                        launch = lambda: L.fold(5, 23, 0, ptr[P], ptr[:P], chunk, st)  # noqa: E731
+                        algo = (P + 1) * nb
+                    else:
+                        launch = lambda: L.prefix(5, 23, ptr[P:2 * P], ptr[:P], chunk, -1, st)  # noqa: E731
+                        algo = 2 * P * nb
+                    for _ in range(3):
+                        launch()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda.synchronize()
+                    e0.record(S)
+                    for _ in range(args.reps):
+                        launch()
+                    e1.record(S)
+                    torch.cuda.synchronize()
+                    t = e0.elapsed_time(e1) / 1e3 / args.reps
+                    gbs = algo / t / 1e9
+                    out.setdefault(f"{kind}/{sname}/{cname}", []).append(round(gbs, 1))
+                    print(f"round {rnd} {kind:>6} {sname:>9} {cname:>5}: {t * 1e3:.4f} ms {gbs:8.1f} GB/s",
+                          file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__" and "--layouts" in sys.argv:
+    sys.argv.remove("--layouts")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    layouts(ap.parse_args())
+    sys.exit(0)
+
+
 if __name__ == "__main__" and "--multi" in sys.argv:
     sys.argv.remove("--multi")
     ap = argparse.ArgumentParser()
