@@ -1,7 +1,8 @@
 """CPU: the -m gpu run grades BASELINE.json's configs first (conftest.py
 pytest_collection_modifyitems), so a cut-short or partly failing driver run still has
 every config's parity result: the golden known answers of configs #1-#5, then the
-full-size configs, then pi_reduce as PE processes, then everything else."""
+full-size configs, then pi_reduce as PE processes, then everything else, and the 12-PE one-GPU team
+check last."""
 import os
 import subprocess
 import sys
@@ -27,3 +28,5 @@ def test_gpu_collection_starts_with_the_configs():
     for cfg in ("#2", "#3", "#4", "#5"):
         assert f"test_gpu_reproduces_golden[{cfg}]" in golden
     assert "test_gpu_pi_reduce_known_answer[2]" in golden
+    # the 12-PE one-GPU team check comes last (conftest.py LAST)
+    assert ids[-1].rsplit("/", 1)[-1].startswith("test_gpu_multipe.py::test_team_check[12-"), ids[-3:]
