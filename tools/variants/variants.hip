@@ -119,6 +119,31 @@ __global__ __launch_bounds__(TPB) void k_combine3_x(T *out, const T *a, const T 
     }
 }
 
+// The default shape with the grid stride and the remainder block's index read once,
+// before the tile loop (k_combine3 re-reads gridDim from the dispatch packet after every
+// tile's store -- the stores may alias it -- and a wave then waits for that scalar load
+// before it can exit).
+template <class T, class OP>
+__global__ __launch_bounds__(kThreads) void k_combine3_h(T *out, const T *a, const T *b, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    const size_t nblk = gridDim.x;
+    const size_t tiles = g.tiles;
+    const u32x4 *A = reinterpret_cast<const u32x4 *>(a + g.head);
+    const u32x4 *B = reinterpret_cast<const u32x4 *>(b + g.head);
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    for (size_t t = blockIdx.x; t < tiles; t += nblk) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        const u32x4 ra = ldv<true>(A + i), rb = ldv<true>(B + i);
+        stv<true>(O + i, apply<T, OP>(ra, rb));
+    }
+    if (g.has_rem && blockIdx.x == nblk - 1) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
+        for (size_t i = g.head + tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            out[i] = OP::f(a[i], b[i]);
+    }
+}
+
 // Tuning variants of k_fold (bench A/B, sosxv_fold): each workgroup takes S
 // consecutive tiles (longer contiguous runs per input stream), optionally loading tile
 // j+1 before storing tile j (PF), optionally with an XCD-contiguous tile order
@@ -199,6 +224,7 @@ const char *const kCombineNames[] = {
     "x1024",             // 17: 1024 threads per workgroup
     "x512_xcd",          // 18
     "x256",              // 19: the k_combine3_x control (same shape as u1_nt)
+    "u1_nt_hoist",       // 20: u1_nt with gridDim read once before the tile loop
 };
 constexpr int kNumCombine = (int)(sizeof(kCombineNames) / sizeof(kCombineNames[0]));
 
@@ -399,6 +425,12 @@ int sosxv_combine(int v, float *out, const float *a, const float *b, size_t n, v
         case 17: return combine_x<1024, 0>(out, a, b, n, st);
         case 18: return combine_x<512, 1>(out, a, b, n, st);
         case 19: return combine_x<256, 0>(out, a, b, n, st);
+        case 20: {
+            Geom g = make_geom((uintptr_t)out, n, sizeof(T), 1);
+            hipLaunchKernelGGL((k_combine3_h<T, OP>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st,
+                               out, a, b, g);
+            return hip_ok(hipGetLastError());
+        }
     }
     return SOSX_ERR_ARG;
 }
