@@ -57,6 +57,25 @@ def test_pi_reduce_multi_pe(examples, np_):
     assert lines == [GOLDEN_PI[np_]], r.stdout
 
 
+@pytest.mark.parametrize("alg", ["auto", "linear", "tree", "recdbl", "ring", "bogus"])
+def test_reduce_algorithm_env_matrix(examples, alg):
+    """SOS's CI runs `make check` once per SHMEM_REDUCE_ALGORITHM = auto, linear, tree,
+    recdbl, ring on 2 processes (.github/workflows/ci.yml:86-124, :246-252).  The same
+    matrix here over the C programs: pi_reduce's golden line (an integer sum, the same under
+    every schedule) and reduce_types' closed forms, 2 PE processes.  linear and tree run
+    recdbl_sw, as SOS does without NIC atomics (src/shmem_collectives.h:200-229); an unknown
+    name is ignored with SOS's warning (src/collectives.c:195-210)."""
+    env = {"SHMEM_REDUCE_ALGORITHM": alg}
+    r = oshrun(2, [os.path.join(examples, "pi_reduce_amd")], timeout=180, extra_env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert [ln for ln in r.stdout.splitlines() if ln.startswith("Pi from")] == [GOLDEN_PI[2]], r.stdout
+    if alg == "bogus":
+        assert "Ignoring bad reduction algorithm 'bogus'" in r.stderr, r.stderr[-2000:]
+    r = oshrun(2, [os.path.join(examples, "reduce_types")], timeout=180, extra_env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert "reduce_types: OK (2 PEs)" in r.stdout
+
+
 def test_reduce_types_4_pes(examples):
     r = oshrun(4, [os.path.join(examples, "reduce_types")], timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
