@@ -76,6 +76,21 @@ def test_reduce_algorithm_env_matrix(examples, alg):
     assert "reduce_types: OK (2 PEs)" in r.stdout
 
 
+@pytest.mark.parametrize("crossover,want", [(None, "ring"), ("1M", "recdbl"), ("32768", "ring"),
+                                            ("32769", "recdbl")])
+def test_coll_size_crossover_env(crossover, want):
+    """SHMEM_COLL_SIZE_CROSSOVER moves AUTO's switch from recdbl_sw to the ring
+    (src/shmem_collectives.h:179-200: recdbl_sw below the crossover, the ring at or above
+    it): a 32 KiB float sum over 4 PE processes gives the ring's bits by default (16 KiB)
+    and at a crossover of exactly 32 KiB, recdbl_sw's bits one byte above; on device-heap
+    operands (the executor) and host-heap ones (the small shared-memory path)."""
+    env = {} if crossover is None else {"SHMEM_COLL_SIZE_CROSSOVER": crossover}
+    r = oshrun(4, [sys.executable, os.path.join(ROOT, "tests", "crossover_pe.py"), want], timeout=180,
+               extra_env=env)
+    ok = re.findall(r"PE (\d)/4: (\w+) bits on device and host heap", r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == [0, 1, 2, 3], r.stdout + r.stderr[-2000:]
+
+
 def test_reduce_types_4_pes(examples):
     r = oshrun(4, [os.path.join(examples, "reduce_types")], timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
