@@ -8,7 +8,9 @@
 //   * 256-thread workgroups, one 4 KiB-per-operand tile per workgroup, >> 256
 //     workgroups per launch (a 128Mi fp32 combine is 131072 workgroups), the ragged
 //     head/tail handled by one extra workgroup so the hot tiles carry no bounds checks;
-//   * relative 16-B misalignment of the operands falls back to element loads.
+//   * `in` at another 16-B offset than inout: the same vectors, each lane funnel-shifting
+//     the two aligned vectors of `in` its bytes straddle (k_combine3_realign); only
+//     operands that are not element-aligned, or inout/out incongruent, take element loads.
 // The shapes this default won against (U, plain loads/stores, persistent grids, LDS-DMA
 // partner tiles, buffer loads, 512/1024-thread workgroups, XCD-contiguous tile order;
 // DESIGN.md section 4) live in the bench-only library tools/variants/.
@@ -16,7 +18,7 @@
 
 namespace sos {
 
-// Relative misalignment between the operands (not 16-B congruent): element loads.
+// Operands not element-aligned, or out and a not 16-B congruent: element loads.
 template <class T, class OP>
 __global__ __launch_bounds__(kThreads) void k_combine3_scalar(T *out, const T *a,
                                                                 const T *b, size_t n)
@@ -48,6 +50,17 @@ int launch_combine3(T *out, const T *a, const T *b, size_t n, hipStream_t st)
     if (n == 0) return SOSX_OK;
     const uintptr_t o = (uintptr_t)out, pa = (uintptr_t)a, pb = (uintptr_t)b;
     const bool congruent = ((o ^ pa) & 15) == 0 && ((o ^ pb) & 15) == 0 && (o % sizeof(T)) == 0;
+    // `in` at another 16-B offset than inout (element-aligned): the realigning kernel,
+    // 6.41-6.63 TB/s at 512 MiB per operand against 2.68-5.13 for element loads
+    // (profiles/r4_misaligned_combine.txt)
+    if (!congruent && sizeof(T) <= 16 && ((o ^ pa) & 15) == 0 && (o % sizeof(T)) == 0 &&
+        (pb % sizeof(T)) == 0) {
+        Geom g = make_geom(o, n, sizeof(T), 1);
+        const unsigned d = (unsigned)((uintptr_t)(b + g.head) & 15);
+        hipLaunchKernelGGL((k_combine3_realign<T, OP>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0,
+                           st, out, a, b, g, d);
+        return hip_ok(hipGetLastError());
+    }
     if (!congruent || sizeof(T) > 16) {
         size_t blocks = (n + kThreads - 1) / kThreads;
         if (blocks > 8192) blocks = 8192;

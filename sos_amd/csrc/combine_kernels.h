@@ -36,4 +36,49 @@ __global__ __launch_bounds__(kThreads) void k_combine3(T *out, const T *a,
     }
 }
 
+// ---------------------------------------------------------------------------------
+// out = a OP b with `b` NOT 16-B congruent with out/a (a caller's sub-array, SOS's
+// reduce_local takes any element alignment): out and a stream as in k_combine3; each
+// lane loads the two 16-B-aligned vectors of b that its 16 bytes straddle and funnel-
+// shifts them into place (v_alignbyte), so every HBM access stays a 16-B vector instead
+// of one element per lane.  `d` = the byte offset of b's vector j within b's aligned
+// vector j (1..15, a multiple of the element alignment).  A 16-B-aligned load that holds
+// at least one byte of b cannot cross a page boundary, and every load here does, so
+// reading the bytes shifted out is safe.  Same element operations as k_combine3.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ u32x4 realign16(const u32x4 &lo, const u32x4 &hi, unsigned d)
+{
+    const unsigned w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    const unsigned q = d >> 2, r = d & 3;
+    unsigned t[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)  // t[j] = w[q + j], q wave-uniform: selects, not scratch
+        t[j] = q == 0 ? w[j] : q == 1 ? w[j + 1] : q == 2 ? w[j + 2] : w[j + 3];
+    u32x4 v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(t[k + 1], t[k], r);
+    return v;
+}
+
+template <class T, class OP>
+__global__ __launch_bounds__(kThreads) void k_combine3_realign(T *out, const T *a, const T *b,
+                                                                 Geom g, unsigned d)
+{
+    constexpr int V = Pack<T>::N;
+    const size_t nblk = gridDim.x;
+    const u32x4 *A = reinterpret_cast<const u32x4 *>(a + g.head);
+    const u32x4 *B = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(b + g.head) - d);
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        const u32x4 ra = ldv<true>(A + i), lo = ldv<true>(B + i), hi = ldv<true>(B + i + 1);
+        stv<true>(O + i, apply<T, OP>(ra, realign16(lo, hi, d)));
+    }
+    if (g.has_rem && blockIdx.x == nblk - 1) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            out[i] = OP::f(a[i], b[i]);
+    }
+}
+
 }  // namespace sos

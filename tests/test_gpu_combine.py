@@ -120,6 +120,28 @@ def test_combine_relatively_misaligned(torch_cuda, sos, oracle, dt, op):
     assert same_bits(from_dev(da, 0, a), ref)
 
 
+@pytest.mark.parametrize("dt,op", [(18, 5), (3, 2), (23, 5), (4, 4), (24, 6), (11, 2), (26, 5)])
+def test_combine_realigned_every_offset(torch_cuda, sos, oracle, dt, op):
+    """`in` at every element-aligned 16-B offset relative to `inout` (the realigning
+    vector kernel, k_combine3_realign), with `inout` itself on and off a 16-B boundary,
+    at sizes from a few elements (head/tail only) to past a million (many tiles); bit for
+    bit against the oracle's reduce_local."""
+    torch = torch_cuda
+    rng = np.random.default_rng(31 + dt)
+    es = oracle.lib().oracle_type_size(dt)
+    for n in (5, 4097, 65536 + 3, (1 << 20) + 7):
+        a, b = make_inputs(oracle, dt, op, n, rng, False)
+        ref = a.copy()
+        oracle.reduce_local(op, dt, b, ref)
+        for a_off in (0, es if es < 16 else 0):
+            for d in range(es, 16, es):
+                da, pa = to_dev(torch, a, a_off)
+                db, pb = to_dev(torch, b, a_off + d)
+                sos.combine(op, dt, pa, pb, n)
+                torch.cuda.synchronize()
+                assert check(dt, op, from_dev(da, a_off, a), ref), f"n={n} a_off={a_off} d={d}"
+
+
 def test_combine3_out_of_place(torch_cuda, sos, oracle):
     torch = torch_cuda
     n = 100003

@@ -1,0 +1,60 @@
+"""Bench-only probe: the local combine (sosx_combine, inout = inout OP in) when the two
+operands are NOT 16-B congruent (in starts `off` bytes past a 16-B boundary, inout on
+one), against the same call on congruent operands.  SOS's reduce_local takes any element
+alignment (src/shmem_internal_op.h:305-339); a caller reducing into a sub-array hits this.
+
+Usage: python tools/misaligned_probe.py [--bytes 536870912] [--reps 20]
+Prints one JSON line: {type/offset: {"ms", "GBs", "frac"}}.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bytes", type=int, default=512 << 20)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+    from sos_amd import _lib as L
+    torch.cuda.set_device(0)
+    S = torch.cuda.current_stream()
+    st = S.cuda_stream
+    nb = a.bytes
+    x = torch.empty(nb + 4096, dtype=torch.uint8, device="cuda")
+    y = torch.empty(nb + 4096 + (1 << 20), dtype=torch.uint8, device="cuda")
+    xa = (x.data_ptr() + 4095) & ~4095
+    ya = ((y.data_ptr() + (1 << 20) - 1) & ~((1 << 20) - 1)) + 4096  # 4 KiB colour apart
+    out = {}
+    for tname, offs in (("float", (0, 4, 8)), ("double", (0, 8)), ("uchar", (0, 1, 3)),
+                        ("short", (0, 2)), ("complexd", (0,))):
+        dt = L.dtype_id(tname)
+        es = L.dtype_size(dt)
+        n = (nb - 64) // es
+        op = L.op_id("sum")
+        for off in offs:
+            b = ya + off
+            L.fill(dt, 0, 0x5EED, 0, xa, n, 0, st)
+            L.fill(dt, 0, 0x5EED, 1, b, n, 0, st)
+            for _ in range(3):
+                L.combine(op, dt, xa, b, n, st)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(S)
+            for _ in range(a.reps):
+                L.combine(op, dt, xa, b, n, st)
+            e1.record(S)
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1) / 1e3 / a.reps
+            gbs = 3 * n * es / t / 1e9
+            out[f"{tname}/+{off}"] = {"ms": round(t * 1e3, 4), "GBs": round(gbs, 1), "frac": round(gbs / 8000, 4)}
+            print(f"{tname:>9} +{off}: {t * 1e3:.4f} ms {gbs:8.1f} GB/s", file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
