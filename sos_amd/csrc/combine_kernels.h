@@ -46,20 +46,6 @@ __global__ __launch_bounds__(kThreads) void k_combine3(T *out, const T *a,
 // at least one byte of b cannot cross a page boundary, and every load here does, so
 // reading the bytes shifted out is safe.  Same element operations as k_combine3.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ u32x4 realign16(const u32x4 &lo, const u32x4 &hi, unsigned d)
-{
-    const unsigned w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    const unsigned q = d >> 2, r = d & 3;
-    unsigned t[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j)  // t[j] = w[q + j], q wave-uniform: selects, not scratch
-        t[j] = q == 0 ? w[j] : q == 1 ? w[j + 1] : q == 2 ? w[j + 2] : w[j + 3];
-    u32x4 v;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(t[k + 1], t[k], r);
-    return v;
-}
-
 template <class T, class OP>
 __global__ __launch_bounds__(kThreads) void k_combine3_realign(T *out, const T *a, const T *b,
                                                                  Geom g, unsigned d)

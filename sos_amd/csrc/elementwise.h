@@ -228,6 +228,24 @@ __device__ __forceinline__ void stv(u32x4 *p, u32x4 v)
     }
 }
 
+// The 16 bytes at offset d (1..15) of the 32-byte concatenation lo || hi: a vector of an
+// operand that is not 16-B congruent with the kernel's grid, from the two aligned
+// vectors its bytes straddle (v_alignbyte_b32; q = d / 4 is wave-uniform, so the dword
+// choice is a uniform branch, not scratch).
+__device__ __forceinline__ u32x4 realign16(const u32x4 &lo, const u32x4 &hi, unsigned d)
+{
+    const unsigned w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    const unsigned q = d >> 2, r = d & 3;
+    unsigned t[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        t[j] = q == 0 ? w[j] : q == 1 ? w[j + 1] : q == 2 ? w[j + 2] : w[j + 3];
+    u32x4 v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_alignbyte(t[k + 1], t[k], r);
+    return v;
+}
+
 constexpr int kThreads = 256;
 
 // Geometry of one (out, a, b) or fold call, computed on the host:

@@ -93,6 +93,60 @@ __global__ __launch_bounds__(kThreads) void k_fold(T *out, FoldPtrs ins, Geom g)
     }
 }
 
+// ---------------------------------------------------------------------------------
+// The ring's LINEAR fold (2 <= P <= 8, at run time) when some inputs are NOT 16-B
+// congruent with the output: a team reduction whose source and target sit at different
+// 16-B offsets (the PE's own source chunk, or the peers' sources read in place, against
+// exchange scratch congruent with the target).  16-B vectors throughout: an input at
+// byte offset d[k] != 0 is read as the two aligned vectors its bytes straddle and
+// funnel-shifted into place (realign16; see k_combine3_realign for why the extra bytes
+// are safe to load).  acc = in[0] OP in[1] OP ... as fold_elem's LINEAR order, with P at
+// run time on compile-time indices, so one kernel per (type, op) serves every P.
+// ---------------------------------------------------------------------------------
+struct FoldRealignArgs {
+    const void *p[8];
+    unsigned d[8];
+    int np;
+};
+
+template <class T, class OP>
+__global__ __launch_bounds__(kThreads) void k_fold_realign(T *out, FoldRealignArgs a, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    const size_t nblk = gridDim.x;
+    const int np = a.np;
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        u32x4 x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k < np) {
+                const unsigned d = a.d[k];
+                const u32x4 *I = reinterpret_cast<const u32x4 *>(
+                    reinterpret_cast<const char *>((const T *)a.p[k] + g.head) - d);
+                const u32x4 lo = ldv<true>(I + i);
+                x[k] = d ? realign16(lo, ldv<true>(I + i + 1), d) : lo;
+            }
+        }
+        u32x4 acc = x[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k)
+            if (k < np) acc = apply<T, OP>(acc, x[k]);
+        stv<true>(O + i, acc);
+    }
+    if (g.has_rem && blockIdx.x == nblk - 1) {
+        auto one = [&](size_t i) {
+            T acc = ((const T *)a.p[0])[i];
+            for (int k = 1; k < np; ++k) acc = OP::f(acc, ((const T *)a.p[k])[i]);
+            out[i] = acc;
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
 constexpr int kMaxPrefix = 64;
 
 struct PrefixPtrs {

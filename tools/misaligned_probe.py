@@ -56,5 +56,49 @@ def main():
     print(json.dumps(out))
 
 
+def fold(args):
+    """The 8-input LINEAR fold (sosx_fold, the ring's local step) over 16Mi fp32 per input:
+    all inputs congruent with the output, input 0 (the PE's own source chunk) at +4 bytes,
+    and every input at +4 (peers' sources read in place, target elsewhere)."""
+    import torch
+    from sos_amd import _lib as L
+    torch.cuda.set_device(0)
+    S = torch.cuda.current_stream()
+    st = S.cuda_stream
+    P, n, es = 8, 16 << 20, 4
+    nb = n * es
+    bufs = [torch.empty(nb + (1 << 20), dtype=torch.uint8, device="cuda") for _ in range(P + 1)]
+    # page-aligned, 4 KiB colours apart (as the device heap places them); 1 MiB of slack
+    base = [((b.data_ptr() + 4095) & ~4095) + 4096 * (k % 8) for k, b in enumerate(bufs)]
+    out = {}
+    for name, offs in (("congruent", [0] * P), ("input0+4", [4] + [0] * (P - 1)), ("all+4", [4] * P)):
+        ins = [base[k] + offs[k] for k in range(P)]
+        for k in range(P):
+            L.fill(23, 0, 0x5EED, k, ins[k], n, 0, st)
+        launch = lambda: L.fold(5, 23, 0, base[P], ins, n, st)  # noqa: E731
+        for _ in range(3):
+            launch()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(S)
+        for _ in range(args.reps):
+            launch()
+        e1.record(S)
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 1e3 / args.reps
+        gbs = (P + 1) * nb / t / 1e9
+        out[name] = {"ms": round(t * 1e3, 4), "GBs": round(gbs, 1), "frac": round(gbs / 8000, 4)}
+        print(f"fold {name:>10}: {t * 1e3:.4f} ms {gbs:8.1f} GB/s", file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__" and "--fold" in sys.argv:
+    sys.argv.remove("--fold")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    fold(ap.parse_args())
+    sys.exit(0)
+
+
 if __name__ == "__main__":
     main()
