@@ -76,6 +76,29 @@ def test_loopback_large_ring_fp32(torch_cuda, sos, oracle):
         assert np.array_equal(db[p].cpu().numpy().view(np.uint32), ref[p].view(np.uint32))
 
 
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("spad,dpad", [(4, 0), (0, 8), (12, 4)])
+def test_loopback_ring_source_target_misaligned(torch_cuda, sos, oracle, P, spad, dpad):
+    """Ring team reductions whose source and target start at different 16-B offsets, with
+    chunks past 64 KiB: the fold's own-chunk input is incongruent with the target and its
+    scratch slots (k_fold_realign); bit for bit with SOS's ring."""
+    from sos_amd import shmem as S
+    torch = torch_cuda
+    for dt, op in ((23, 5), (11, 2), (3, 4)):
+        n = (1 << 20) + 5
+        srcs = [oracle.fill(dt, 0, 77 + dt, p, n) for p in range(P)]
+        ref = oracle.ring(op, dt, srcs)
+        es = srcs[0].itemsize
+        sp, dp = (spad // es) * es, (dpad // es) * es
+        sb = [dev_bytes(torch, s, sp) for s in srcs]
+        db = [torch.zeros(n * es + dp + 64, dtype=torch.uint8, device="cuda") for _ in range(P)]
+        S.loopback_allreduce("ring", op, dt, [b.data_ptr() + sp for b in sb], [b.data_ptr() + dp for b in db], n)
+        torch.cuda.synchronize()
+        for p in range(P):
+            got = host_view(db[p], dp, srcs[p])
+            assert np.array_equal(got.view(np.uint8), ref[p].view(np.uint8)), (P, dt, op, sp, dp, p)
+
+
 @pytest.fixture(scope="module")
 def shmem1(torch_cuda, sos):
     from sos_amd import shmem as S
