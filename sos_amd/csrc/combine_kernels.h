@@ -57,7 +57,8 @@ __global__ __launch_bounds__(kThreads) void k_combine3_realign(T *out, const T *
     u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
     for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
         const size_t i = t * (size_t)kThreads + threadIdx.x;
-        const u32x4 ra = ldv<true>(A + i), lo = ldv<true>(B + i), hi = ldv<true>(B + i + 1);
+        const u32x4 ra = ldv<true>(A + i), lo = ldv<true>(B + i);
+        const u32x4 hi = ldv<true>(B + i + 1);
         stv<true>(O + i, apply<T, OP>(ra, realign16(lo, hi, d)));
     }
     if (g.has_rem && blockIdx.x == nblk - 1) {
