@@ -188,6 +188,27 @@ struct PrefixFn {
         // the vector kernels serve the team scans, which are sums (shmemx_<T>_sum_inscan /
         // _exscan); other ops take the element loop (sosx_prefix accepts them all)
         if constexpr (std::is_same<OP, OpSum>::value) {
+            if (!congruent && np <= 8 && sizeof(T) <= 16 && (o % sizeof(T)) == 0) {
+                // outputs congruent, some inputs at other 16-B offsets (element-aligned):
+                // 16-B vectors, the inputs realigned in registers
+                bool outs_ok = true;
+                for (int k = 0; k < np; ++k)
+                    outs_ok &= (((uintptr_t)p->out[k] ^ o) & 15) == 0 && ((uintptr_t)p->in[k] % sizeof(T)) == 0;
+                if (outs_ok) {
+                    Geom g = make_geom(o, n, sizeof(T), 1);
+                    PrefixRealignArgs a;
+                    memset(&a, 0, sizeof(a));
+                    a.np = np;
+                    for (int k = 0; k < np; ++k) {
+                        a.in[k] = p->in[k];
+                        a.out[k] = p->out[k];
+                        a.d[k] = (unsigned)((uintptr_t)((const T *)p->in[k] + g.head) & 15);
+                    }
+                    hipLaunchKernelGGL((k_prefix_realign<T, OP>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0,
+                                       st, a, g);
+                    return hip_ok(hipGetLastError());
+                }
+            }
             if (congruent) {
                 switch (np) {
                     case 1: return launch_prefix_np<T, OP, 1>(*p, n, st);

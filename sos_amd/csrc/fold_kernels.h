@@ -203,4 +203,67 @@ __global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
     }
 }
 
+// The team scan's prefix (1 <= P <= 8, at run time) when some INPUTS sit at another 16-B
+// offset than the outputs (a scan whose source and target are at different offsets: the
+// PE's own source chunk against target-congruent scratch); the outputs are congruent.
+// Inputs realigned as in k_fold_realign; every input vector of a tile is loaded before
+// the first store, as in k_prefix (an output may alias an input: the aliased pair is
+// congruent, so it is never read past its own vector).
+struct PrefixRealignArgs {
+    const void *in[8];
+    void *out[8];
+    unsigned d[8];
+    int np;
+};
+
+template <class T, class OP>
+__global__ __launch_bounds__(kThreads) void k_prefix_realign(PrefixRealignArgs a, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    const size_t nblk = gridDim.x;
+    const int np = a.np;
+    for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        u32x4 x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k < np) {
+                const unsigned d = a.d[k];
+                const u32x4 *I = reinterpret_cast<const u32x4 *>(
+                    reinterpret_cast<const char *>((const T *)a.in[k] + g.head) - d);
+                const u32x4 lo = ldv<true>(I + i);
+                x[k] = d ? realign16(lo, ldv<true>(I + i + 1), d) : lo;
+            }
+        }
+        u32x4 acc = x[0];
+        stv<true>(reinterpret_cast<u32x4 *>((T *)a.out[0] + g.head) + i, acc);
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+            if (k < np) {
+                acc = apply<T, OP>(acc, x[k]);
+                stv<true>(reinterpret_cast<u32x4 *>((T *)a.out[k] + g.head) + i, acc);
+            }
+        }
+    }
+    if (g.has_rem && blockIdx.x == nblk - 1) {
+        auto one = [&](size_t i) {
+            T v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = k < np ? ((const T *)a.in[k])[i] : T();
+            T acc = v[0];
+            ((T *)a.out[0])[i] = acc;
+#pragma unroll
+            for (int k = 1; k < 8; ++k) {
+                if (k < np) {
+                    acc = OP::f(acc, v[k]);
+                    ((T *)a.out[k])[i] = acc;
+                }
+            }
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
 }  // namespace sos

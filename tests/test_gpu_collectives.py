@@ -69,6 +69,27 @@ def test_prefix_kernel(torch_cuda, np_, dt):
             assert np.array_equal(bits(from_dev(do[k], ref[k])), bits(ref[k])), (np_, n, k)
 
 
+@pytest.mark.parametrize("np_", [1, 2, 3, 8])
+@pytest.mark.parametrize("dt", [23, 24, 4, 1, 27])
+def test_prefix_realigned_inputs(torch_cuda, np_, dt):
+    """SUM prefix whose inputs sit at other 16-B offsets than its (congruent) outputs
+    (k_prefix_realign: a scan with source and target at different offsets), input 0 only
+    or every input at its own offset, ragged sizes; bit for bit against the in-order
+    prefix of the oracle's reduce_local."""
+    torch = torch_cuda
+    es = O.lib().oracle_type_size(dt)
+    for n in (999, (1 << 18) + 5):
+        ins = [src_of(dt, n + 7, k, n) for k in range(np_)]
+        ref = cpu_prefix(5, dt, ins)
+        for offs in ([es % 16] + [0] * (np_ - 1), [(es * (k + 1)) % 16 for k in range(np_)]):
+            di = [to_dev(torch, a, off) for a, off in zip(ins, offs)]
+            do = [torch.zeros_like(to_dev(torch, a)) for a in ins]
+            _lib.prefix(5, dt, [t.data_ptr() for t in do], [t.data_ptr() + off for t, off in zip(di, offs)], n)
+            torch.cuda.synchronize()
+            for k in range(np_):
+                assert np.array_equal(bits(from_dev(do[k], ref[k])), bits(ref[k])), (np_, n, offs, k)
+
+
 @pytest.mark.parametrize("np_", [3, 8, 12])
 def test_prefix_kernel_aliasing(torch_cuda, np_):
     """An in-place exscan: output k-1 is input k's buffer.  np <= 8 may alias any input;
