@@ -76,6 +76,33 @@ int main(void)
     shmemx_free_device(ddst);
     shmemx_free_device(dsrc);
 
+    /* sub-arrays at different 16-B offsets on device memory: an int sum of M elements from
+       src + 3 into dst + 1 (the realigning kernels), and reduce_local between the two */
+    enum { M = 300007 };
+    int *isrc = shmemx_malloc_device((M + 8) * sizeof(int)), *idst = shmemx_malloc_device((M + 8) * sizeof(int));
+    int *hv = malloc((M + 8) * sizeof(int));
+    for (size_t i = 0; i < M; i++) hv[i] = (int) (i % 1000) * (me + 1) - 7 * me;
+    hipMemcpy(isrc + 3, hv, M * sizeof(int), hipMemcpyHostToDevice);
+    shmem_int_sum_reduce(SHMEM_TEAM_WORLD, idst + 1, isrc + 3, M);
+    hipMemcpy(hv, idst + 1, M * sizeof(int), hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < M && !bad; i++) {
+        int x = 0;
+        for (int p = 0; p < np; p++) x += (int) (i % 1000) * (p + 1) - 7 * p;
+        if (hv[i] != x) bad = fail("int_sum_reduce(misaligned sub-arrays)", i);
+    }
+    /* idst + 1 += isrc + 3 (inout and in at different 16-B offsets) */
+    if (shmemx_reduce_local(SOSX_OP_SUM, SOSX_DT_INT, M, isrc + 3, idst + 1) != SOSX_OK)
+        bad = fail("reduce_local status", 0);
+    hipMemcpy(hv, idst + 1, M * sizeof(int), hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < M && !bad; i++) {
+        int x = (int) (i % 1000) * (me + 1) - 7 * me;
+        for (int p = 0; p < np; p++) x += (int) (i % 1000) * (p + 1) - 7 * p;
+        if (hv[i] != x) bad = fail("reduce_local(misaligned sub-arrays)", i);
+    }
+    free(hv);
+    shmemx_free_device(idst);
+    shmemx_free_device(isrc);
+
     shmem_barrier_all();
     if (me == 0 && !bad) printf("reduce_types: OK (%d PEs)\n", np);
     shmem_finalize();
