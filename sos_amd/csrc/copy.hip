@@ -68,7 +68,8 @@ __global__ __launch_bounds__(kMaxSig) void k_p2p_signal(SigArgs a) { sig_step(a,
 struct GatherArgs {
     const char *src[kMaxSeg];
     char *dst[kMaxSeg];
-    uint64_t head[kMaxSeg];    // bytes before the 16-B aligned body
+    uint64_t head[kMaxSeg];    // bytes before the 16-B aligned body (of dst)
+    unsigned sd[kMaxSeg];      // src's offset within its aligned vectors there (0: congruent)
     uint64_t nvec[kMaxSeg];    // 16-B vectors in the body
     uint64_t bytes[kMaxSeg];
     uint64_t tstart[kMaxSeg + 1];  // prefix sums of each segment's tiles
@@ -98,15 +99,26 @@ __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g, Sig<kMaxGate>
     if (t < g.tstart[g.nseg]) {
         int s = 0;
         while (t >= g.tstart[s + 1]) ++s;
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(g.src[s] + g.head[s]);
+        const unsigned sd = g.sd[s];
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(g.src[s] + g.head[s] - sd);
         u32x4 *dst = reinterpret_cast<u32x4 *>(g.dst[s] + g.head[s]);
         const uint64_t j0 = (t - g.tstart[s]) * kTileVec + threadIdx.x;
         const uint64_t nv = g.nvec[s];
         u32x4 v[kGatherU];
+        if (sd == 0) {
 #pragma unroll
-        for (int u = 0; u < kGatherU; ++u) {
-            const uint64_t j = j0 + (uint64_t)u * kThreads;
-            if (j < nv) v[u] = __builtin_nontemporal_load(src + j);
+            for (int u = 0; u < kGatherU; ++u) {
+                const uint64_t j = j0 + (uint64_t)u * kThreads;
+                if (j < nv) v[u] = __builtin_nontemporal_load(src + j);
+            }
+        } else {  // src at another 16-B offset: two aligned vectors, funnel-shifted
+#pragma unroll
+            for (int u = 0; u < kGatherU; ++u) {
+                const uint64_t j = j0 + (uint64_t)u * kThreads;
+                if (j < nv)
+                    v[u] = realign16(__builtin_nontemporal_load(src + j),
+                                     __builtin_nontemporal_load(src + j + 1), sd);
+            }
         }
 #pragma unroll
         for (int u = 0; u < kGatherU; ++u) {
@@ -171,15 +183,14 @@ int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size
             g.src[n] = (const char *)srcs[i];
             g.dst[n] = (char *)dsts[i];
             g.bytes[n] = bytes[i];
-            if (((s ^ d) & 15) == 0) {
-                uint64_t h = (16 - (d & 15)) & 15;
-                if (h > bytes[i]) h = bytes[i];
-                g.head[n] = h;
-                g.nvec[n] = (bytes[i] - h) / 16;
-            } else {
-                g.head[n] = bytes[i];  // incongruent: all bytes by the byte loop
-                g.nvec[n] = 0;
-            }
+            // the body on dst's 16-B grid; an incongruent src is realigned in registers
+            // (every load is a 16-B-aligned block holding at least one byte of the
+            // segment, so none crosses a page the segment does not touch)
+            uint64_t h = (16 - (d & 15)) & 15;
+            if (h > bytes[i]) h = bytes[i];
+            g.head[n] = h;
+            g.nvec[n] = (bytes[i] - h) / 16;
+            g.sd[n] = (unsigned)((s + h) & 15);
             g.tstart[n] = tot;
             tot += (g.nvec[n] + kTileVec - 1) / kTileVec;
             ++n;

@@ -228,11 +228,11 @@ def test_loopback_reduce_twelve_pes(torch_cuda, alg):
             assert np.array_equal(bits(got[p]), bits(ref[p])), (alg, n, p)
 
 
-@pytest.mark.parametrize("case", ["allgather8", "ragged", "incongruent", "many", "tiny"])
+@pytest.mark.parametrize("case", ["allgather8", "ragged", "incongruent", "incongruent_many", "many", "tiny"])
 def test_gather_kernel(torch_cuda, case):
     """sosx_gather (the p2p transport's multi-segment copy, copy.hip k_gather): one tile
-    per workgroup over the 16-B congruent bodies, byte loops for the ragged ends and for
-    segments whose source and destination are not 16-B congruent; more than 16 segments
+    per workgroup over the 16-B bodies on the destination's grid (a source at another 16-B
+    offset realigned in registers), byte loops for the ragged ends; more than 16 segments
     split into several launches.  Every destination byte must equal its source byte, and
     bytes around the segments stay untouched."""
     import ctypes
@@ -246,6 +246,9 @@ def test_gather_kernel(torch_cuda, case):
         segs = [(1, 2, 100000), (5, 0, 33), (0, 7, 70000)]
     elif case == "many":
         segs = [(int(rng.integers(0, 16)),) * 2 + (int(rng.integers(1, 200000)),) for _ in range(37)]
+    elif case == "incongruent_many":  # every src/dst offset pair, bodies realigned in registers
+        segs = [(int(rng.integers(0, 16)), int(rng.integers(0, 16)), int(rng.integers(1, 1 << 20)))
+                for _ in range(23)]
     else:
         segs = [(0, 0, 1), (15, 15, 15), (4, 9, 0)]
     srcs, dsts, sp, dp, nb = [], [], [], [], []
