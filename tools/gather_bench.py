@@ -20,13 +20,18 @@ def main():
     ap.add_argument("--n", type=int, default=128 << 20, help="nreduce (fp32 elements per PE)")
     ap.add_argument("--P", type=int, default=8)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--src-offset", type=int, default=0,
+                    help="bytes past a 16-B boundary for every source (incongruent with the "
+                         "destinations when not a multiple of 16)")
     a = ap.parse_args()
     import torch
     from sos_amd import _lib as L
     torch.cuda.set_device(0)
     seg = a.n // a.P * 4
     nseg = a.P - 1
-    src = [torch.empty(seg, dtype=torch.uint8, device="cuda") for _ in range(nseg)]
+    off = a.src_offset
+    srcbuf = [torch.empty(seg + 64, dtype=torch.uint8, device="cuda") for _ in range(nseg)]
+    src = [b[off:off + seg] for b in srcbuf]
     dst = [torch.empty(seg, dtype=torch.uint8, device="cuda") for _ in range(nseg)]
     for k, b in enumerate(src):
         L.fill(L.dtype_id("float"), L.DIST_UNIFORM, 0x5EED, k, b.data_ptr(), seg // 4)
@@ -43,7 +48,7 @@ def main():
         for s_, d_ in zip(src, dst):
             d_.copy_(s_, non_blocking=True)
 
-    out = {"P": a.P, "segments": nseg, "segment_bytes": seg,
+    out = {"P": a.P, "segments": nseg, "segment_bytes": seg, "src_offset": off,
            "bytes_moved_per_launch": 2 * nseg * seg}
     for name, fn in (("k_gather", gather), ("runtime_d2d_copies", runtime_copy)):
         for _ in range(3):
