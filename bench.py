@@ -20,6 +20,9 @@ sample of the same workload.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--sweep]
        torchrun --nproc-per-node N bench.py --gpus N   (N > 1)
+       python bench.py --gpus N   (N > 1, no launcher: bench.py starts the N rank
+                                   processes itself and prints rank 0's line)
+--gpus N must equal the launcher's WORLD_SIZE when there is one (exit 2 otherwise).
 """
 import argparse
 import csv
@@ -76,6 +79,8 @@ def parse():
     p.add_argument("--fold-p", type=int, default=8,
                    help="inputs of the fold / prefix kernel legs (one PE's chunk of a P-PE call)")
     p.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--launch-check", action="store_true",
+                   help="N > 1 plumbing only: gloo group + rank 0 prints the ranks (no GPU)")
     a = p.parse_args()
     a.n = a.nreduce
     return a
@@ -652,13 +657,111 @@ def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
 
 
 # ----------------------------------------------------------------------------------
+# --gpus N > 1 without a launcher: this process spawns the N rank processes itself
+# ----------------------------------------------------------------------------------
+def free_port_base(span=16):
+    """A port p with p .. p+span-1 free on 127.0.0.1 (the team leg uses MASTER_PORT, the
+    shmem bootstrap MASTER_PORT + 1 and the preflight job MASTER_PORT + 12)."""
+    import random
+    import socket
+    for _ in range(200):
+        base = random.randint(20000, 60000 - span)
+        socks = []
+        try:
+            for k in range(span):
+                s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+                socks.append(s)
+                s.bind(("127.0.0.1", base + k))
+            return base
+        except OSError:
+            continue
+        finally:
+            for s in socks:
+                s.close()
+    raise RuntimeError("no free port range on 127.0.0.1")
+
+
+def spawn_ranks(n, argv, grace_s=60.0):
+    """Run `bench.py argv` as n rank processes (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT set as torch.distributed.run sets them), one per GPU.
+    This parent never touches the GPU: it only starts the ranks, passes their stderr
+    through, forwards rank 0's one JSON line to stdout and returns the worst exit code.
+    When a rank fails, the others get `grace_s` to finish before they are killed (by
+    PID).  Returns (rc, rank 0's JSON line or None)."""
+    port = free_port_base()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                    "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0",
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = []
+    import threading
+    reader = threading.Thread(target=lambda: out0.extend(procs[0].stdout.read().decode().splitlines()),
+                              daemon=True)
+    reader.start()
+    failed_at = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            break
+        if failed_at is None and any(rc not in (None, 0) for rc in rcs):
+            failed_at = time.time()
+            log(f"[spawn] a rank exited with {[rc for rc in rcs if rc not in (None, 0)]}; "
+                f"waiting up to {grace_s:.0f} s for the others")
+        if failed_at is not None and time.time() - failed_at > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    reader.join(timeout=30)
+    rcs = [p.returncode for p in procs]
+    lines = [ln for ln in out0 if ln.startswith("{")]
+    rc = next((c for c in rcs if c != 0), 0)
+    if rc == 0 and len(lines) != 1:
+        log(f"[spawn] rank 0 printed {len(lines)} JSON lines, expected one")
+        rc = 1
+    return rc, (lines[0] if lines else None)
+
+
+def launch_check(torch):
+    """--launch-check (CPU, no GPU touched): every rank joins a gloo group from the
+    launcher's environment and rank 0 prints the ranks it saw -- the plumbing of the
+    N > 1 line without the library (tests/test_bench_launch.py)."""
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    seen = [None] * world
+    dist.all_gather_object(seen, {"rank": rank, "local_rank": int(os.environ["LOCAL_RANK"]),
+                                  "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": seen}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
 def main():
     args = parse()
-    import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1 and not args.child_pmc:
+        # no launcher: run the N ranks from here (a line for N GPUs or none at all)
+        rc, line = spawn_ranks(args.gpus, sys.argv[1:])
+        if line is not None and rc == 0:
+            print(line, flush=True)
+        return rc
+    world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus and not args.child_pmc:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        # never report an N-GPU figure measured on another number of ranks
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}: run with a matching launcher "
+            f"(or none: bench.py --gpus N spawns its N ranks itself)")
+        return 2
+    import torch
+    if args.launch_check:
+        return launch_check(torch)
     if (world > 1 or args.team) and not args.child_pmc:
         sys.path.insert(0, os.path.join(HERE, "tools"))
         import team_bench   # the N > 1 leg (bench code: tools/team_bench.py)

@@ -223,6 +223,15 @@ int sosx_set_rccl_allgather(int on);
  * value.  Collective switch; returns the previous mode, -1 if out of range. */
 int sosx_set_rccl_allreduce(int mode);
 
+/* The rank count of the job's RCCL communicator (ncclCommCount), or -1 when the job has
+ * none (p2p transport only, or a single PE).  Introspection for benchmarks. */
+int sosx_rccl_comm_count(void);
+
+/* Free this PE's private device workspaces (exchange scratch and the staging buffer of
+ * host operands) once the library stream has drained; the next call that needs one
+ * allocates it again.  Local (not collective).  Returns the bytes released. */
+size_t sosx_release_workspaces(void);
+
 /* The p2p transport's mapping flags (introspection for tests): the hipHostRegister
  * flags of the shared pair-counter segment and the hipIpcOpenMemHandle flags of a peer's
  * device heap. */

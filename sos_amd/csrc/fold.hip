@@ -54,14 +54,28 @@ __global__ __launch_bounds__(kThreads) void k_fold_dyn(T *out, FoldPtrs ins, int
 
 // ---------------------------------------------------------------------------------
 // Fused prefix (the team scan's local step): outs[k] = ins[0] OP ... OP ins[k].
-// P inputs, P outputs, one pass: 2*P*n*s HBM bytes.  NP <= 8: every input of a vector
-// is loaded before the first store (any output may alias any input).  Larger P: a
-// runtime loop; the one input that may alias an output (`own`, the PE's own source
-// chunk under an in-place scan) is loaded before any store.
+// P inputs, P outputs, one pass: 2*P*n*s HBM bytes.  P <= 8 (vector kernels and the
+// element loop alike): every input of an element is loaded before the first store, so
+// any output may alias any input.  Larger P: the one input that may alias an output
+// (`own`, the PE's own source chunk under an in-place scan) is loaded before any store.
 // ---------------------------------------------------------------------------------
 template <class T, class OP>
 __device__ __forceinline__ void prefix_elem_dyn(const PrefixPtrs &p, int np, int own, size_t i)
 {
+    if (np <= 8) {
+        T v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = k < np ? ((const T *)p.in[k])[i] : T();
+        T acc = v[0];
+        ((T *)p.out[0])[i] = acc;
+#pragma unroll
+        for (int k = 1; k < 8; ++k)
+            if (k < np) {
+                acc = OP::f(acc, v[k]);
+                ((T *)p.out[k])[i] = acc;
+            }
+        return;
+    }
     const T ov = own >= 0 ? ((const T *)p.in[own])[i] : T();
     T acc = own == 0 ? ov : ((const T *)p.in[0])[i];
     ((T *)p.out[0])[i] = acc;

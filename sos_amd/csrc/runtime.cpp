@@ -296,17 +296,23 @@ void *Heap::alloc(size_t bytes, size_t align)
     bytes = (bytes + 255) & ~(size_t)255;
     const bool colour = device && bytes >= kColorMin && align <= kColorStep;
     const size_t want = colour ? (size_t)(colour_seq % (kColorPeriod / kColorStep)) * kColorStep : 0;
-    for (auto it = free_blocks.begin(); it != free_blocks.end(); ++it) {
-        size_t off = it->first, len = it->second;
-        size_t aoff = (off + align - 1) / align * align;
-        if (colour) aoff += (want + kColorPeriod - aoff % kColorPeriod) % kColorPeriod;
-        if (aoff + bytes > off + len) continue;
-        free_blocks.erase(it);
-        if (aoff > off) free_blocks[off] = aoff - off;
-        if (off + len > aoff + bytes) free_blocks[aoff + bytes] = off + len - (aoff + bytes);
-        used_blocks[aoff] = bytes;
-        if (colour) ++colour_seq;
-        return base + aoff;
+    // first fit at the colour; when no free block holds the coloured placement (a heap
+    // sized tightly), first fit without it: the colour is a rate preference, never a
+    // reason to fail.  The choice depends only on the allocation sequence, so it is the
+    // same on every PE and offsets stay symmetric.
+    for (int pass = colour ? 0 : 1; pass < 2; ++pass) {
+        for (auto it = free_blocks.begin(); it != free_blocks.end(); ++it) {
+            size_t off = it->first, len = it->second;
+            size_t aoff = (off + align - 1) / align * align;
+            if (pass == 0) aoff += (want + kColorPeriod - aoff % kColorPeriod) % kColorPeriod;
+            if (aoff + bytes > off + len) continue;
+            free_blocks.erase(it);
+            if (aoff > off) free_blocks[off] = aoff - off;
+            if (off + len > aoff + bytes) free_blocks[aoff + bytes] = off + len - (aoff + bytes);
+            used_blocks[aoff] = bytes;
+            if (colour) ++colour_seq;
+            return base + aoff;
+        }
     }
     return nullptr;
 }
@@ -990,6 +996,33 @@ int sosx_set_rccl_allgather(int on)
     const int prev = s.rccl_allgather ? 1 : 0;
     s.rccl_allgather = on != 0;
     return prev;
+}
+
+// The rank count RCCL's own communicator reports (ncclCommCount), or -1 when this job has
+// no RCCL communicator (p2p-only, or one PE): what a bench line names so a reader can see
+// that RCCL, and not only the launcher, saw every PE.
+int sosx_rccl_comm_count(void)
+{
+    State &s = st();
+    int n = -1;
+    if (!s.comm || ncclCommCount(s.comm, &n) != ncclSuccess) return -1;
+    return n;
+}
+
+// Return this PE's private device workspaces (exchange scratch, staging for host
+// operands) to the runtime after the library stream drains; the next call that needs one
+// allocates it afresh.  Local, not collective.  Returns the bytes released.
+size_t sosx_release_workspaces(void)
+{
+    State &s = st();
+    if (!s.initialized) return 0;
+    hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize");
+    const size_t had = (s.scratch ? s.scratch_bytes : 0) + (s.stage ? s.stage_bytes : 0);
+    if (s.scratch) hip_check(hipFree(s.scratch), "hipFree(scratch)");
+    if (s.stage) hip_check(hipFree(s.stage), "hipFree(stage)");
+    s.scratch = s.stage = nullptr;
+    s.scratch_bytes = s.stage_bytes = 0;
+    return had;
 }
 
 // RCCL executor: world-team reductions as one ncclAllReduce where RCCL has the type and

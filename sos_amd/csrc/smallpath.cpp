@@ -281,7 +281,10 @@ long small_path_calls() { return g.calls; }
 long small_path_device_calls() { return g.dev_calls; }
 
 // Collective over the world when the job is up: every PE passes the same limit (checked
-// through the bootstrap), so the path choice for device operands stays uniform.
+// through the bootstrap), so the path choice for device operands stays uniform.  Without
+// the bootstrap hub (shmemx_init_attr) there is no node shared segment, so the small
+// path never sets up (small_path_setup returns at once) and the limit routes nothing:
+// a disagreement there cannot split a call between paths, and no check is needed.
 size_t small_path_set_device_bytes(size_t team_bytes)
 {
     State &s = st();

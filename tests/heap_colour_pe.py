@@ -32,6 +32,16 @@ def main():
     assert (after - big[-1]) % 8192 == 4096, (after - big[-1]) % 32768
     for p in big + [after, small]:
         L.shmemx_free_device(p)
+    # a heap filled to capacity: the whole region (SHMEMX_DEVICE_HEAP_SIZE minus the stage
+    # region) in one allocation fits only without the colour padding, which it then goes
+    # without instead of failing
+    region = int(os.environ["HEAP_REGION_BYTES"])
+    full = S.shmemx_malloc_device(region)
+    assert full == big[0], (full, big[0])
+    L.shmemx_free_device(full)
+    again = S.shmemx_malloc_device(64 << 20)   # the colours go on after the fallback
+    assert again and (again - big[0]) % 32768 == 4096 * 4, (again - big[0]) % 32768
+    L.shmemx_free_device(again)
     print(f"PE {me}: colours {cols} offsets {offs}", flush=True)
     S.shmem_finalize()
     return 0

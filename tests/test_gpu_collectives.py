@@ -91,18 +91,21 @@ def test_prefix_realigned_inputs(torch_cuda, np_, dt):
 
 
 @pytest.mark.parametrize("np_", [3, 8, 12])
-def test_prefix_kernel_aliasing(torch_cuda, np_):
-    """An in-place exscan: output k-1 is input k's buffer.  np <= 8 may alias any input;
-    larger np names the aliased input `own` (one per call)."""
+@pytest.mark.parametrize("op", [5, 4, 6])
+def test_prefix_kernel_aliasing(torch_cuda, np_, op):
+    """An in-place exscan: output k-1 is input k's buffer.  np <= 8 may alias any input,
+    for every op (SUM through the vector kernel, MAX/PROD through the element loop, which
+    loads every input of an element before its first store); larger np names the aliased
+    input `own` (one per call)."""
     torch = torch_cuda
     dt, n = 24, 4099
     ins = [src_of(dt, 5, k, n) for k in range(np_)]
-    ref = cpu_prefix(5, dt, ins)
+    ref = cpu_prefix(op, dt, ins)
     j = np_ // 2
     di = [to_dev(torch, a) for a in ins]
     do = [torch.zeros_like(t) for t in di]
     do[j - 1] = di[j]  # output j-1 overwrites input j
-    _lib.prefix(5, dt, [t.data_ptr() for t in do], [t.data_ptr() for t in di], n,
+    _lib.prefix(op, dt, [t.data_ptr() for t in do], [t.data_ptr() for t in di], n,
                 own=j if np_ > 8 else -1)
     torch.cuda.synchronize()
     for k in range(np_):

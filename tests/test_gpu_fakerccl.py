@@ -179,6 +179,25 @@ def test_bench_team_leg_rccl():
         assert curve[-1]["bitwise_mismatches_all_ranks"] == 0   # 4Mi: equal chunks
 
 
+def test_bench_spawns_ranks_without_launcher():
+    """`python bench.py --gpus 2` with no launcher environment (as the driver may call it):
+    bench.py starts both rank processes itself, and the one line says n_gpus 2 with the
+    communicator's rank count (the stand-in's ncclCommCount) 2 on both ranks."""
+    env = _env()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "2", "--warmup", "1", "--no-cpu", "--no-host", "--no-adjacent",
+                        "--no-team-sweep", "--no-small", "--no-pmc", "--nreduce", str((1 << 20) + 3)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    _used_fake(r, 2)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["rccl_comm_ranks"] == [2, 2], res
+    assert res["check"]["bitwise_mismatches_all_ranks"] == 0
+    assert abs(res["algbw_GiBs"] * 2 - res["value"]) < 0.01 * res["value"], res
+
+
 def test_bench_rccl_allreduce_is_checked_by_tolerance():
     """Four PEs: RCCL's own allreduce order (the stand-in folds in rank order) differs
     from SOS's ring for fp sum, so rccl_ar shows bitwise mismatches, stays inside the fp

@@ -183,3 +183,16 @@ def test_workload_names_the_device_map():
     assert "8 PEs on 1 GPU (shared" in shared and "1 per MI355X" not in shared
     assert TB.parallelism_text(8, 8) == "pe8" and TB.parallelism_text(8, 1) == "pe8_on_1gpu"
     assert "4 PEs on 2 GPUs (shared" in TB.workload_text("p2p", "float", "sum", 8, 4, 2)
+
+
+def test_headline_fields_n2():
+    """The N > 1 line's rate fields at N = 2 with a 2-rank RCCL communicator (what the
+    stand-in's ncclCommCount reports): value = both PEs' payload per step, algbw_GiBs =
+    one PE's vector per step, the definition stated in the line."""
+    f = TB.headline_fields(2, 1 << 20, 4, 0.001, [2, 2])
+    assert f["n_gpus"] == 2 and f["rccl_comm_ranks"] == [2, 2]
+    assert abs(f["value"] - 2 * 4 * (1 << 20) / 0.001 / TB.GiB) < 1e-3
+    assert abs(f["algbw_GiBs"] * 2 - f["value"]) < 1e-2
+    assert "1->8 scaling curve plots this" in f["value_definition"]
+    none = TB.headline_fields(2, 8, 4, None, [-1, -1])
+    assert none["value"] is None and none["algbw_GiBs"] is None and none["rccl_comm_ranks"] == [-1, -1]

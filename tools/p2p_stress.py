@@ -50,6 +50,10 @@ def main():
     ap.add_argument("--n", type=int, default=(1 << 20) + 3)
     ap.add_argument("--n2", type=int, default=65536)
     ap.add_argument("--alg", default="recdbl_gather")
+    ap.add_argument("--release", action="store_true",
+                    help="every iteration starts from released workspaces and runs a small call "
+                         "first, so each big call is the first after its scratch grew (hipFree + "
+                         "hipMalloc), the condition of the round-4 failure, every iteration")
     a = ap.parse_args()
     S.shmem_init()
     me, P = S.shmem_my_pe(), S.shmem_n_pes()
@@ -63,8 +67,23 @@ def main():
     fn = S.shmem_float_sum_reduce
     prev = None      # every PE's hsrc contents before this iteration's fill
     bad, checks = [], 0
+    grows = 0
     for it in range(a.iters):
         seed = 0x51A000 + it
+        if a.release:
+            L.lib().sosx_release_workspaces()
+            # a small heap call: the scratch is allocated at its (small) size first
+            t1 = O.fill(dt, 0, seed + 3, me, n2)
+            L.check(L.lib().sosx_memcpy(hsrc, t1.ctypes.data, n2 * 4, None), "sosx_memcpy")
+            fn(world, hdst, hsrc, n2)
+            e1 = O.recdbl(op, dt, [O.fill(dt, 0, seed + 3, q, n2) for q in range(P)])[me]
+            checks += 1
+            m1 = int(np.count_nonzero(download(hdst, n2 * 4).view(np.uint32) != e1.view(np.uint32)))
+            if m1:
+                bad.append({"iter": it, "mode": "small_first", "mismatches": m1})
+            grows += 1
+        if me == 0 and it % 10 == 0:
+            print(f"[p2p_stress] iteration {it}/{a.iters}", file=sys.stderr, flush=True)
         ins = [O.fill(dt, 0, seed, q, n) for q in range(P)]
         exp = O.recdbl(op, dt, ins)[me]
         for mode in ("heap", "heap_inplace"):
@@ -112,7 +131,8 @@ def main():
     if bad:
         print(f"PE {me}/{P}: {len(bad)} of {checks} FAILED: {bad[:4]}", flush=True)
         return 1
-    print(f"PE {me}/{P}: {checks} checks OK ({a.alg}, n={n}, {a.iters} iterations)", flush=True)
+    print(f"PE {me}/{P}: {checks} checks OK ({a.alg}, n={n}, {a.iters} iterations, "
+          f"{grows} calls right after a scratch grow)", flush=True)
     return 0
 
 

@@ -62,6 +62,26 @@ SCHEDULE_T = ("rccl", "rccl_ag", "p2p", "p2p_host")
 # even where its bits happen to equal SOS's ring (integer ops, fp sum at P = 2).
 VALUE_T = SCHEDULE_T
 
+# What `value` is at every N, stated in the line itself: the
+# payload of ALL PEs per step, the same definition as the N = 1 line (one PE's payload).
+VALUE_DEFINITION = ("value = N * nreduce * sizeof(T) / max-over-ranks step time (whole-job "
+                    "payload; the 1->8 scaling curve plots this); algbw_GiBs = nreduce * "
+                    "sizeof(T) / step time (one PE's vector per step, NCCL's algbw)")
+
+
+def headline_fields(world, n, es, t_step, rccl_ranks):
+    """The line's rate fields (t_step None: no clean transport).  `value` is the whole-job
+    payload per step (every PE's nreduce * sizeof(T)), the N = 1 line's definition at N = 1;
+    algbw_GiBs is one PE's vector per step; rccl_comm_ranks is what every rank's RCCL
+    communicator reported (ncclCommCount; -1 without RCCL)."""
+    ok = t_step is not None and t_step > 0
+    return {"value": round(world * n * es / t_step / GiB, 3) if ok else None,
+            "unit": "GiB/s",
+            "algbw_GiBs": round(n * es / t_step / GiB, 3) if ok else None,
+            "value_definition": VALUE_DEFINITION,
+            "n_gpus": world,
+            "rccl_comm_ranks": list(rccl_ranks)}
+
 
 def select_primary(results):
     """(transport `value` comes from, None) or (None, reason).  Only a VALUE_T transport
@@ -197,6 +217,9 @@ def main(args, torch, pmc=None):
     ngpus = len(set(idents))
     S.shmem_init()
     assert S.shmem_n_pes() == world and S.shmem_my_pe() == rank
+    # the rank count RCCL's communicator reports (-1: no RCCL in this job), every rank's
+    rccl_ranks = [None] * world
+    dist.all_gather_object(rccl_ranks, int(L.lib().sosx_rccl_comm_count()))
     alg = L.ALGS[args.alg]
     S.shmemx_set_reduce_algorithm(alg)
 
@@ -319,6 +342,7 @@ def main(args, torch, pmc=None):
         ts = rr["t_step"]
         return {"ms_per_step": round(ts * 1e3, 4),
                 "value_GiBs": round(world * n * es / ts / GiB, 3),
+                "algbw_GiBs": round(n * es / ts / GiB, 3),
                 "busbw_GBs": round(wire / ts / 1e9, 1),
                 "frac_one_link": round(wire / ts / 1e9 / XGMI_LINK_GBS, 3),
                 "frac_7_links": round(wire / ts / 1e9 / (XGMI_LINK_GBS * XGMI_LINKS), 3),
@@ -334,9 +358,7 @@ def main(args, torch, pmc=None):
     fold_ms = r["prof"]["fold_ms"] / max(r["prof"]["nfold"], 1) if r else 0.0
     res = {
         "metric": "GiB/s device-resident sum_reduce combine, nreduce=128Mi fp32; 1/2/4/8 GPU",
-        "value": round(world * n * es / t_step / GiB, 3) if r else None,
-        "unit": "GiB/s",
-        "n_gpus": world,
+        **headline_fields(world, n, es, t_step, rccl_ranks),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(t_step * 1e3, 4) if r else None,
