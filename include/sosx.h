@@ -232,6 +232,12 @@ int sosx_rccl_comm_count(void);
  * allocates it again.  Local (not collective).  Returns the bytes released. */
 size_t sosx_release_workspaces(void);
 
+/* System-scope completion markers issued so far: every call that returns data (and every
+ * p2p post) first records an event with hipEventReleaseToSystem on the library stream, so
+ * its device stores are in HBM -- visible to DMA reads, the host and peer GPUs -- when the
+ * call returns.  Introspection for tests. */
+long sosx_sys_releases(void);
+
 /* The p2p transport's mapping flags (introspection for tests): the hipHostRegister
  * flags of the shared pair-counter segment and the hipIpcOpenMemHandle flags of a peer's
  * device heap. */

@@ -98,6 +98,7 @@ _SIGS = {
     "sosx_set_rccl_allreduce": (_c.c_int, [_c.c_int]),
     "sosx_rccl_comm_count": (_c.c_int, []),
     "sosx_release_workspaces": (_c.c_size_t, []),
+    "sosx_sys_releases": (_c.c_long, []),
     "sosx_gather": (_c.c_int, [_c.c_int, _c.POINTER(_c.c_void_p), _c.POINTER(_c.c_void_p),
                                _c.POINTER(_c.c_size_t), _c.c_void_p]),
 }

@@ -297,7 +297,7 @@ void execute_p2p(const Plan &p, const Team &t, int alg, size_t count, size_t ts,
     // (its target may be pageable memory: a full stream synchronisation)
     if (!direct && p.writes_dst) {
         hip_check(hipMemcpyAsync(target, s.sym_stage, bytes, hipMemcpyDefault, s.stream), "stage out");
-        hip_check(hipStreamSynchronize(s.stream), fn);
+        hip_check(sync_system(s.stream), fn);
     }
     if (g_prof.on) g_prof.collect();
 }
@@ -365,7 +365,7 @@ bool striped_host_ring(int alg, void *target, const void *source, size_t count, 
         hip_check(hipStreamCreateWithFlags(&s.pipe_d2h, hipStreamNonBlocking), "hipStreamCreate");
         for (auto &slot : s.pipe_ev)
             for (hipEvent_t &e : slot)
-                hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+                hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToSystem), "hipEventCreate");
     }
     enum { H2D = 0, XCH = 1, D2H = 2 };
     const size_t nfull = (q + L - 1) / L;
@@ -451,8 +451,8 @@ bool striped_host_ring(int alg, void *target, const void *source, size_t count, 
         copy_slices(slot, dst, first, len, np, false, s.pipe_d2h);
         hip_check(hipEventRecord(s.pipe_ev[sl][D2H], s.pipe_d2h), "stripe event");
     }
-    hip_check(hipStreamSynchronize(s.pipe_d2h), fn);
-    hip_check(hipStreamSynchronize(s.stream), fn);
+    hip_check(sync_system(s.pipe_d2h), fn);
+    hip_check(sync_system(s.stream), fn);
     if (g_prof.on) g_prof.collect();
     return true;
 }
@@ -523,7 +523,7 @@ void execute(int alg, void *target, const void *source, size_t count, size_t ts,
         if (g_prof.on) (void)hipEventRecord(g_prof.get(g_prof.xfer_ev, g_prof.nx, true), s.stream);
         if (!dev_dst)
             hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
-        hip_check(hipStreamSynchronize(s.stream), fn);
+        hip_check(sync_system(s.stream), fn);
         if (g_prof.on) g_prof.collect();
         return;
     }
@@ -537,7 +537,7 @@ void execute(int alg, void *target, const void *source, size_t count, size_t ts,
     if (rc) raise_error("%s: %s", fn, status_text(rc));
     if (!dev_dst && p.writes_dst)
         hip_check(hipMemcpyAsync(target, ddst, bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
-    hip_check(hipStreamSynchronize(s.stream), fn);
+    hip_check(sync_system(s.stream), fn);
     if (g_prof.on) g_prof.collect();
 }
 
@@ -552,7 +552,7 @@ void op_to_all(void *target, const void *source, size_t count, size_t ts, const 
         // PE_size 1: copy (src/collectives.c:664-668), no combine, any datatype
         if (target != source)
             hip_check(hipMemcpyAsync(target, source, bytes, hipMemcpyDefault, s.stream), fn);
-        hip_check(hipStreamSynchronize(s.stream), fn);
+        hip_check(sync_system(s.stream), fn);
         return;
     }
     int rc = sos_check_op(op, dt);
@@ -815,7 +815,7 @@ int shmemx_reduce_local(int op, int datatype, size_t count, const void *in, void
             return SOSX_ERR_HIP;
     }
     if (rc) return rc;
-    return hipStreamSynchronize(s.stream) == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
+    return sync_system(s.stream) == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
 }
 
 // ---- phase timing -----------------------------------------------------------------
@@ -918,7 +918,7 @@ int sosx_loopback_allreduce(int alg, int P, int op, int datatype, void *const *s
             return SOSX_ERR_ARG;  // deadlock: inconsistent plans
         }
     }
-    hipError_t e = hipStreamSynchronize(sm);
+    hipError_t e = sync_system(sm);
     if (g_prof.on) {
         g_prof.ncall++;
         g_prof.collect();

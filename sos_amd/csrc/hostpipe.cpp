@@ -65,7 +65,7 @@ int setup(size_t slot_bytes)
                   hipStreamCreateWithFlags(&p.s_out, hipStreamNonBlocking) == hipSuccess;
         for (int i = 0; ok && i < Pipe::kSlots; ++i)
             ok = hipEventCreateWithFlags(&p.in_done[i], hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&p.cmp_done[i], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&p.cmp_done[i], hipEventDisableTiming | hipEventReleaseToSystem) == hipSuccess &&
                  hipEventCreateWithFlags(&p.out_done[i], hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             release();

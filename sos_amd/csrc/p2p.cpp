@@ -375,6 +375,9 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
     std::map<const uint64_t *, uint64_t> pw_wait;
     auto flush = [&]() -> int {
         if (pw_store.empty() && pw_wait.empty()) return SOSX_OK;
+        // posts make the bytes of this round's sends readable by peers, on other GPUs
+        // over xGMI: a system-scope release in stream order first (release_system)
+        if (!pw_store.empty() && release_system(stream) != hipSuccess) return SOSX_ERR_HIP;
         std::vector<uint64_t *> wa;
         std::vector<uint64_t> wv;
         std::vector<const uint64_t *> qa;
@@ -433,7 +436,7 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
             first_xfer_round = false;
             bool sends = false;
             for (const auto &x : r.xfers) sends |= x.send != 0;
-            if (sends && hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
+            if (sends && sync_system(stream) != hipSuccess) return SOSX_ERR_HIP;
             host_flush();
             stall_hook();
         } else {
@@ -495,6 +498,7 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
             }
             pw_store.clear();
             pw_wait.clear();
+            if (!wa.empty() && release_system(stream) != hipSuccess) return SOSX_ERR_HIP;
             prof_mark(1, false, stream);
             rc = sosx_gather_signalled((int)gs.size(), gs.data(), gd.data(), gb.data(),
                                        (int)wa.size(), wa.data(), wv.data(), (int)qa.size(),
@@ -534,7 +538,7 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
     }
     // the exit boundary (the last round's consumed marks) on the host, after the sync
     phase(PH_ENQUEUE);
-    const hipError_t e = hipStreamSynchronize(stream);
+    const hipError_t e = sync_system(stream);
     if (__atomic_load_n(&sh->sig_err[my_world], __ATOMIC_ACQUIRE))
         raise_error("p2p transport: timed out after %.0f s waiting for a peer (device wait)",
                     wait_limit_s());
@@ -691,7 +695,9 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
         bool any_send = false;
         for (const auto &x : r.xfers) any_send |= x.send != 0;
         if (any_send) {
-            if (hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
+            // the sent bytes must be in HBM, not only complete: peers on other GPUs read
+            // them over xGMI, which no L2 of this GPU serves (system-scope release)
+            if (sync_system(stream) != hipSuccess) return SOSX_ERR_HIP;
             phase(PH_SYNC_SEND);
             for (const auto &x : r.xfers)
                 if (x.send) {
@@ -776,7 +782,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
             if (rc) return rc;
         }
     }
-    const hipError_t e = hipStreamSynchronize(stream);
+    const hipError_t e = sync_system(stream);  // the caller's result in HBM (sync_system)
     phase(PH_SYNC_END);
     if (tr && ++g_trace.calls % g_trace.every == 0) {  // window averages, then reset
         const double k = 1e6 / (double)g_trace.every;

@@ -476,6 +476,25 @@ static void *grow(void **buf, size_t *have, size_t need, const char *what)
     return *buf;
 }
 
+hipError_t release_system(hipStream_t stream)
+{
+    State &s = st();
+    if (!s.sys_ev) {
+        const hipError_t e =
+            hipEventCreateWithFlags(&s.sys_ev, hipEventReleaseToSystem | hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    ++s.sys_releases;
+    return hipEventRecord(s.sys_ev, stream);
+}
+
+hipError_t sync_system(hipStream_t stream)
+{
+    hipError_t e = release_system(stream);
+    if (e == hipSuccess) e = hipEventSynchronize(st().sys_ev);
+    return e;
+}
+
 void *scratch(size_t bytes) { return grow(&st().scratch, &st().scratch_bytes, bytes, "hipMalloc(scratch)"); }
 void *stage(size_t bytes) { return grow(&st().stage, &st().stage_bytes, bytes, "hipMalloc(stage)"); }
 
@@ -540,7 +559,7 @@ void team_barrier(const Team &t)
     if (s.shm.base) {
         // node-local: the stream first (SOS barrier also completes outstanding work),
         // then the shared-memory arrival counters of this member set
-        hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize(barrier)");
+        hip_check(sync_system(s.stream), "hipStreamSynchronize(barrier)");
         if (t.size > 1 && t.my_idx >= 0 && !s.shm.wait(t.start, t.stride, t.size, 600.0))
             raise_error("barrier timed out (team start %d stride %d size %d)", t.start, t.stride,
                         t.size);
@@ -556,7 +575,7 @@ void team_barrier(const Team &t)
             nccl_check(ncclGroupEnd(), "ncclGroupEnd");
         }
     }
-    hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize(barrier)");
+    hip_check(sync_system(s.stream), "hipStreamSynchronize(barrier)");
 }
 
 Team *team_from_handle(shmem_team_t handle) { return reinterpret_cast<Team *>(handle); }
@@ -781,6 +800,8 @@ void shmem_finalize(void)
             if (e) (void)hipEventDestroy(e);
             e = nullptr;
         }
+    if (s.sys_ev) (void)hipEventDestroy(s.sys_ev);
+    s.sys_ev = nullptr;
     for (hipStream_t *ps : {&s.pipe_h2d, &s.pipe_d2h}) {
         if (*ps) (void)hipStreamDestroy(*ps);
         *ps = nullptr;
@@ -1009,6 +1030,10 @@ int sosx_rccl_comm_count(void)
     return n;
 }
 
+// How many system-scope completion markers (sync_system / release_system) this PE has
+// issued: every call that returns data ends with one (introspection for tests).
+long sosx_sys_releases(void) { return st().sys_releases; }
+
 // Return this PE's private device workspaces (exchange scratch, staging for host
 // operands) to the runtime after the library stream drains; the next call that needs one
 // allocates it afresh.  Local, not collective.  Returns the bytes released.
@@ -1056,7 +1081,7 @@ void shmem_sync_all(void) { shmem_barrier_all(); }
 
 void shmem_quiet(void)
 {
-    if (st().initialized) hip_check(hipStreamSynchronize(st().stream), "hipStreamSynchronize");
+    if (st().initialized) hip_check(sync_system(st().stream), "hipStreamSynchronize");
 }
 
 void shmem_fence(void) { shmem_quiet(); }

@@ -85,6 +85,8 @@ struct State {
     // per-slot events, three device stripe slots (the RCCL path's; p2p uses the stage)
     hipStream_t pipe_h2d = nullptr, pipe_d2h = nullptr;
     hipEvent_t pipe_ev[3][3] = {};    // [slot][h2d done, exchange done, d2h done]
+    hipEvent_t sys_ev = nullptr;      // system-scope release marker (sync_system)
+    long sys_releases = 0;            // how many sync_system / release_system markers ran
     void *stripes = nullptr;
     size_t stripes_bytes = 0;
     size_t host_stripe_bytes = 256u << 10; // SHMEMX_HOST_STRIPE_BYTES: min slice (0 = off)
@@ -143,6 +145,18 @@ size_t env_size(const char *name, size_t dflt);
 void hip_check(hipError_t e, const char *what);
 
 void nccl_check(ncclResult_t r, const char *what);
+
+// Completion with a SYSTEM-scope release: record an event created with
+// hipEventReleaseToSystem on `stream` and wait for it.  The marker's release writes every
+// XCD's L2 back to memory, so what the stream's kernels stored is in HBM when this
+// returns: visible to DMA reads (hipMemcpy on any stream, the host), to peer GPUs reading
+// over xGMI and to other processes.  A plain hipStreamSynchronize only promises the
+// kernels finished; under multi-process queue time-slicing their nontemporal stores were
+// seen still in L2 by a following DMA read ("The 12-PE wrong
+// results").  Every call returns, and every p2p post is made, after this.
+hipError_t sync_system(hipStream_t stream);
+// The same release in stream order, without a host wait (stream-mode p2p posts).
+hipError_t release_system(hipStream_t stream);
 
 // Device workspaces (grown, never shrunk).
 void *scratch(size_t bytes);

@@ -182,7 +182,7 @@ void wait_flags(const uint32_t *flags, int nb, uint32_t seq, const char *fn)
         const hipError_t e = hipStreamQuery(st().stream);
         if (e == hipSuccess) {  // drained: every flag must be visible by now (after the
                                 // runtime's own synchronisation at the latest)
-            hip_check(hipStreamSynchronize(st().stream), fn);
+            hip_check(sync_system(st().stream), fn);
             for (int k = b; k < nb; ++k)
                 if (__atomic_load_n(flags + k, __ATOMIC_ACQUIRE) != seq)
                     raise_error("%s: small shared-memory path: workgroup %d of %d did not "
@@ -519,7 +519,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
             rc = sosx_small_linear(op, dt, out, in, np, count, g.flags, g.fseq, &nblocks, s.stream);
         } else if (dev_dst) {
             hip_check(hipMemsetAsync(out, 0, bytes, s.stream), fn);
-            hip_check(hipStreamSynchronize(s.stream), fn);
+            hip_check(sync_system(s.stream), fn);
         } else {
             memset(out, 0, bytes);
         }
@@ -543,7 +543,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     if (rc) raise_error("%s: small-path reduction failed (status %d)", fn, rc);
     // no fold launch followed the copy kernel (an active-set broadcast's root, exscan's
     // PE 0 with a host target): the call must not return while it still reads `source`
-    if (staged && nblocks == 0) hip_check(hipStreamSynchronize(s.stream), fn);
+    if (staged && nblocks == 0) hip_check(sync_system(s.stream), fn);
     phase(3);
     // 4. completion from the workgroups' flags (no stream synchronisation); then the
     //    peers' slots are read: acknowledge; my result out

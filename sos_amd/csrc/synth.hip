@@ -143,11 +143,22 @@ int sosx_fill(int dtype, int dist, uint64_t seed, int pe, void *dst, size_t coun
     return hip_ok(hipGetLastError());
 }
 
+// Test/bench helper: a system-scope release (an event created with
+// hipEventReleaseToSystem) so that earlier kernel stores are in HBM for the copy's DMA
+// reads, the copy, and the same release after it (a device destination written by a
+// blit kernel is then in HBM for a following DMA read; see sync_system in runtime.h).
 int sosx_memcpy(void *dst, const void *src, size_t bytes, void *stream)
 {
+    static hipEvent_t ev = nullptr;
     hipStream_t st = as_stream(stream);
-    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    hipError_t e = ev ? hipSuccess
+                      : hipEventCreateWithFlags(&ev, hipEventReleaseToSystem | hipEventDisableTiming);
+    // what kernels stored before (on any stream) in HBM first, then the copy
+    if (e == hipSuccess) e = hipEventRecord(ev, st);
+    if (e == hipSuccess) e = hipEventSynchronize(ev);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st);
+    if (e == hipSuccess) e = hipEventRecord(ev, st);
+    if (e == hipSuccess) e = hipEventSynchronize(ev);
     return hip_ok(e);
 }
 

@@ -25,6 +25,7 @@ import torch  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from sos_amd import _lib as L  # noqa: E402
 from sos_amd import shmem as S  # noqa: E402
+from tests import readback as R  # noqa: E402
 
 SCAN_TYPES = ["float", "double", "int", "char", "long", "complexd", "uint8"]
 BCAST_TYPES = ["int", "double", "uint8", "longdouble", "size"]
@@ -37,13 +38,6 @@ def gen(dt, seed, pe, n, es):
     if n:
         L.fill(dt, L.DIST_UNIFORM, seed, pe, b.data_ptr(), n)
     return b
-
-
-def download(ptr, nbytes):
-    t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-    L.check(L.lib().sosx_memcpy(t.data_ptr(), ptr, nbytes, None), "sosx_memcpy")
-    return t[:nbytes]
 
 
 def upload(dst_ptr, t):
@@ -60,16 +54,16 @@ class Buffers:
 
     def run(self, mode, src_dev, init_dst, call):
         """Place src (device tensor) and the target's initial bytes, call(dst, src),
-        return the target's bytes as a device tensor."""
+        return the target's bytes as a host (numpy) copy, read back by tests/readback.py."""
         nb = self.nbytes
         if mode in ("heap", "heap_inplace"):
             upload(self.hsrc, src_dev[:nb])
             if mode == "heap":
                 upload(self.hdst, init_dst[:nb])
                 call(self.hdst, self.hsrc)
-                return download(self.hdst, nb)
+                return R.device_bytes(self.hdst, nb)
             call(self.hsrc, self.hsrc)
-            return download(self.hsrc, nb)
+            return R.device_bytes(self.hsrc, nb)
         if mode == "hostheap":
             hs, hd = self.hh
             a_in = src_dev[:nb].cpu().numpy()      # kept alive across the memmoves
@@ -77,18 +71,17 @@ class Buffers:
             ctypes.memmove(hs, a_in.ctypes.data, nb)
             ctypes.memmove(hd, a_init.ctypes.data, nb)
             call(hd, hs)
-            out = np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(hd)).copy()
-            return torch.from_numpy(out).cuda()
+            return np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(hd)).copy()
         if mode == "device":
             s = src_dev[:nb].clone()
             d = init_dst[:nb].clone()
             torch.cuda.synchronize()
             call(d.data_ptr(), s.data_ptr())
-            return d
+            return R.device_bytes(d.data_ptr(), nb)
         h_in = src_dev[:nb].cpu().numpy().copy()
         h_out = init_dst[:nb].cpu().numpy().copy()
         call(h_out.ctypes.data, h_in.ctypes.data)
-        return torch.from_numpy(h_out).cuda()
+        return h_out
 
 
 def main():
@@ -135,14 +128,14 @@ def main():
                     mine = gen(dt, seed, members[idx], n, es)
                     cpu_ins = [O.fill(dt, L.DIST_UNIFORM, seed, members[i], n) for i in range(m)]
                     ref = O.scan(L.op_id("sum"), dt, cpu_ins, kind == "exscan")[idx]
-                    exp = torch.from_numpy(np.frombuffer(ref.tobytes(), np.uint8).copy()).cuda()
+                    exp = R.as_bytes(ref)
                     zero = torch.zeros_like(mine)
                     for mode in ("heap", "heap_inplace", "device", "host", "hostheap"):
                         if mode in ("host", "hostheap") and n > 5003:
                             continue
                         got = Buffers(hsrc, hdst, n * es, hh).run(
                             mode, mine, zero, lambda d, s: fn(team, d, s, n))
-                        mm = L.count_mismatch(exp.data_ptr(), got.data_ptr(), n, es)
+                        mm = R.mismatches(exp, got, es)
                         check(mm == 0, (tname, kind, ty, n, mode, mm))
         # ---- typed / mem broadcasts -----------------------------------------------------
         for ty in BCAST_TYPES + ["mem"]:
@@ -154,7 +147,7 @@ def main():
                 for root in sorted({0, m - 1, m // 2}):
                     seed = zlib.crc32(f"{tname}/b/{ty}/{n}/{root}".encode())
                     src = gen(L.DTYPES["uchar"], seed, members[idx], n * es, 1)
-                    rsrc = gen(L.DTYPES["uchar"], seed, members[root], n * es, 1)
+                    rsrc = O.fill(L.DTYPES["uchar"], L.DIST_UNIFORM, seed, members[root], n * es)
                     init = torch.full_like(src, SENTINEL)
                     for mode in ("heap", "heap_inplace", "device", "host", "hostheap"):
                         if mode in ("host", "hostheap") and n > 5003:
@@ -162,7 +155,7 @@ def main():
                         got = Buffers(hsrc, hdst, n * es, hh).run(
                             mode, src, init, lambda d, s: fn(team, d, s, n, root))
                         # every PE ends with the root's data (the root copies too)
-                        mm = L.count_mismatch(rsrc.data_ptr(), got.data_ptr(), n * es, 1)
+                        mm = R.mismatches(rsrc, got, 1)
                         check(mm == 0, (tname, "bcast", ty, n, root, mode, mm))
     # ---- active-set broadcast32/64: the root's target is left untouched -------------------
     for bits_, fn in ((32, S.shmem_broadcast32), (64, S.shmem_broadcast64)):
@@ -171,15 +164,15 @@ def main():
             for root in sorted({0, P - 1}):
                 seed = zlib.crc32(f"as/{bits_}/{n}/{root}".encode())
                 src = gen(L.DTYPES["uchar"], seed, me, n * es, 1)
-                rsrc = gen(L.DTYPES["uchar"], seed, root, n * es, 1)
+                rsrc = O.fill(L.DTYPES["uchar"], L.DIST_UNIFORM, seed, root, n * es)
                 init = torch.full_like(src, SENTINEL)
                 for mode in ("heap", "device", "host", "hostheap"):
                     if mode in ("host", "hostheap") and n > 5003:
                         continue
                     got = Buffers(hsrc, hdst, n * es, hh).run(
                         mode, src, init, lambda d, s: fn(d, s, n, root, 0, 0, P, psync))
-                    exp = init[:n * es] if me == root else rsrc
-                    mm = L.count_mismatch(exp.data_ptr(), got.data_ptr(), n * es, 1)
+                    exp = np.full(n * es, SENTINEL, np.uint8) if me == root else rsrc
+                    mm = R.mismatches(exp, got, 1)
                     check(mm == 0, ("active_set", bits_, n, root, mode, mm))
     S.shmem_barrier_all()
     S.shmemx_free_device(hdst)

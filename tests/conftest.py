@@ -26,17 +26,10 @@ def pytest_configure(config):
 # has graded every config before anything else.  Then config #1 as the reference runs it,
 # examples/pi_reduce.c as separate PE processes.
 FIRST = ("test_golden.py", "test_gpu_configs.py", "test_gpu_multipe.py::test_pi_reduce_multi_pe")
-# ... and the 12-PE one-GPU team check runs last: it is the one case that returned a wrong
-# result once in round 4 ("Open"), so under -x a recurrence cannot
-# hide the tests behind it; it still fails the run.
-LAST = ("test_gpu_multipe.py::test_team_check[12-",)
 
 
 def collection_rank(nodeid):
     tail = nodeid.rsplit("/", 1)[-1]
-    for prefix in LAST:
-        if tail.startswith(prefix):
-            return len(FIRST) + 1
     for i, prefix in enumerate(FIRST):
         if tail == prefix or tail.startswith(prefix + "::") or tail.startswith(prefix + "["):
             return i

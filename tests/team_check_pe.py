@@ -25,6 +25,7 @@ import torch  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from sos_amd import _lib as L  # noqa: E402
 from sos_amd import shmem as S  # noqa: E402
+from tests import readback as R  # noqa: E402
 
 CASES = [("float", "sum"), ("double", "prod"), ("int64", "xor"), ("int", "max"), ("complexd", "prod"),
          ("short", "sum"), ("uint8", "min"), ("ulong", "or")]
@@ -45,7 +46,7 @@ def expected(dt, opid, dist, seed, members, my_idx, n, alg_resolved, pe_of):
         out = O.ring(opid, dt, ins)[my_idx]
     else:
         out = O.recdbl(opid, dt, ins)[my_idx]
-    return torch.from_numpy(np.frombuffer(out.tobytes(), np.uint8).copy()).cuda()
+    return R.as_bytes(out)
 
 
 def main():
@@ -102,26 +103,22 @@ def main():
                         fn(world, t_out.data_ptr(), t_in.data_ptr(), n)
                         out = t_out.data_ptr()
                     elif mode == "host":
-                        h_in = _download(hsrc, n * es)
+                        h_in = R.device_bytes(hsrc, n * es)
                         h_out = np.zeros_like(h_in)
                         fn(world, h_out.ctypes.data, h_in.ctypes.data, n)
-                        tmp = torch.from_numpy(h_out).cuda()
-                        torch.cuda.synchronize()
-                        out = tmp.data_ptr()
+                        out = h_out
                     else:
-                        h_in = _download(hsrc, n * es)      # (keep the array alive)
+                        h_in = R.device_bytes(hsrc, n * es)      # (keep the array alive)
                         ctypes.memmove(hh_in, h_in.ctypes.data, n * es)
                         fn(world, hh_out, hh_in, n)
-                        h_out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * es)).from_address(hh_out))
-                        tmp = torch.from_numpy(h_out.copy()).cuda()
-                        torch.cuda.synchronize()
-                        out = tmp.data_ptr()
+                        out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * es)).from_address(hh_out)).copy()
                     if exp is None:
                         exp = expected(dt, opid, dist, seed, list(range(P)), me, n, resolved, lambda i: i)
-                    mm = L.count_mismatch(exp.data_ptr(), out, n, es)
+                    got = out if isinstance(out, np.ndarray) else R.device_bytes(out, n * es)
+                    mm = R.mismatches(exp, got, es)
                     checks += 1
                     if mm:
-                        bad.append((alg, tname, oname, n, mode, mm, _where(exp, out, n, es)))
+                        bad.append((alg, tname, oname, n, mode, mm, _where(exp, got, out, n, es)))
                 # split team: even PEs reduce among themselves
                 if even.value and n <= 5003:
                     L.fill(dt, dist, seed, me, hsrc, n)
@@ -130,18 +127,16 @@ def main():
                     m = (P + 1) // 2
                     exp = expected(dt, opid, dist, seed, list(range(m)), me // 2, n, resolved,
                                    lambda i: 2 * i)
-                    mm = L.count_mismatch(exp.data_ptr(), hdst, n, es)
+                    mm = R.mismatches(exp, R.device_bytes(hdst, n * es), es)
                     checks += 1
                     if mm:
                         bad.append((alg, tname, oname, n, "even_team", mm))
                     # the same team on the host symmetric heap (small host-resident path)
-                    h_in = _download(hsrc, n * es)
+                    h_in = R.device_bytes(hsrc, n * es)
                     ctypes.memmove(hh_in, h_in.ctypes.data, n * es)
                     fn(even.value, hh_out, hh_in, n)
                     h_out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * es)).from_address(hh_out))
-                    tmp = torch.from_numpy(h_out.copy()).cuda()
-                    torch.cuda.synchronize()
-                    mm = L.count_mismatch(exp.data_ptr(), tmp.data_ptr(), n, es)
+                    mm = R.mismatches(exp, h_out.copy(), es)
                     checks += 1
                     if mm:
                         bad.append((alg, tname, oname, n, "even_team_hostheap", mm))
@@ -160,7 +155,7 @@ def main():
                 seed = zlib.crc32(f"persp/{alg}/{tname}/{oname}/{n}".encode())
                 ins = [_perspective(O.fill(dt, L.DIST_UNIFORM, seed, pe, n), pe) for pe in range(P)]
                 exp_np = O.recdbl(opid, dt, ins)[me]
-                exp = torch.from_numpy(np.frombuffer(exp_np.tobytes(), np.uint8).copy()).cuda()
+                exp = R.as_bytes(exp_np)
                 mine = np.frombuffer(ins[me].tobytes(), np.uint8).copy()
                 for mode in ("heap", "hostheap", "host"):
                     if mode == "heap":
@@ -170,16 +165,13 @@ def main():
                     elif mode == "hostheap":
                         ctypes.memmove(hh_in, mine.ctypes.data, n * es)
                         fn(world, hh_out, hh_in, n)
-                        h_out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * es)).from_address(hh_out))
-                        tmp = torch.from_numpy(h_out.copy()).cuda()
-                        out = tmp.data_ptr()
+                        out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * es)).from_address(hh_out)).copy()
                     else:
                         h_out = np.zeros_like(mine)
                         fn(world, h_out.ctypes.data, mine.ctypes.data, n)
-                        tmp = torch.from_numpy(h_out).cuda()
-                        out = tmp.data_ptr()
-                    torch.cuda.synchronize()
-                    mm = L.count_mismatch(exp.data_ptr(), out, n, es)
+                        out = h_out
+                    got = out if isinstance(out, np.ndarray) else R.device_bytes(out, n * es)
+                    mm = R.mismatches(exp, got, es)
                     checks += 1
                     if mm:
                         bad.append(("perspective", alg, tname, oname, n, mode, mm))
@@ -230,31 +222,12 @@ def _perspective(a, pe):
     return a
 
 
-def _where(exp, out, n, es):
+def _where(exp, got, out, n, es):
     """Diagnostics of a mismatch: the differing elements as [first, last) runs (at most 4),
-    and the count of a second comparison of the same bytes after a device synchronisation
-    (a different count means the target changed after the call returned)."""
-    torch.cuda.synchronize()
-    again = L.count_mismatch(exp.data_ptr(), out, n, es)
-    got = _download(out, n * es).reshape(n, es)
-    want = exp.cpu().numpy().reshape(n, es)
-    diff = np.nonzero((got != want).any(axis=1))[0]
-    runs = []
-    if diff.size:
-        cuts = np.nonzero(np.diff(diff) != 1)[0]
-        starts = np.concatenate(([diff[0]], diff[cuts + 1]))
-        ends = np.concatenate((diff[cuts], [diff[-1]])) + 1
-        runs = [(int(a), int(b)) for a, b in zip(starts[:4], ends[:4])]
-        runs.append(f"{starts.size} runs")
-    return {"recount": int(again), "runs": runs}
-
-
-def _download(ptr, nbytes):
-    """Host copy of `nbytes` of device memory at `ptr` (a heap address)."""
-    t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-    _hip_copy(t.data_ptr(), ptr, nbytes)
-    return t.cpu().numpy()
+    and, for a device result, the count of a second readback (a different count means the
+    bytes changed after the call returned)."""
+    again = R.mismatches(exp, R.device_bytes(out, n * es), es) if not isinstance(out, np.ndarray) else None
+    return {"recount": again, "runs": R.diff_runs(exp, got, es)}
 
 
 def _hip_copy(dst, src, nbytes):

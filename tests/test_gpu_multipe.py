@@ -252,6 +252,18 @@ def test_device_heap_colours():
     assert "colours [0, 1, 2, 3, 4, 5, 6, 7, 0, 1]" in lines[0], lines
 
 
+@pytest.mark.parametrize("np_", [2, 3])
+def test_calls_end_with_system_release(np_):
+    """Every executor call (reductions under four schedules in both p2p signalling modes, a
+    scan, a broadcast, reduce_local, a barrier) issues a system-scope release before it
+    returns, so its results are in HBM for DMA reads, the host and peer GPUs (DESIGN.md
+    section 5, the 12-PE wrong results); each result is the oracle's."""
+    r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", "sys_release_pe.py")], timeout=180)
+    ok = re.findall(r"PE (\d+)/\d+: (\d+) calls, each ended with a system-scope release", r.stdout)
+    assert r.returncode == 0 and sorted(int(p) for p, _ in ok) == list(range(np_)), \
+        r.stdout + r.stderr[-2000:]
+
+
 def test_small_device_setter_is_collective():
     """sosx_set_small_device_bytes with different limits on two PEs is refused."""
     r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "route_mismatch_pe.py"), "setter"],

@@ -16,6 +16,7 @@ Usage: tools/oshrun -np 12 python tools/p2p_stress.py [--iters 60] [--n 1048579]
 import argparse
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -33,6 +34,26 @@ def download(ptr, nbytes):
     L.check(L.lib().sosx_memcpy(t.data_ptr(), ptr, nbytes, None), "sosx_memcpy")
     torch.cuda.synchronize()
     return t.cpu().numpy()
+
+
+_PINNED = {}
+
+
+def direct_pinned(ptr, nbytes):
+    """Host copy of device memory by ONE D2H copy into pinned host memory (a DMA read of
+    HBM, no runtime staging buffer)."""
+    t = _PINNED.get(nbytes)
+    if t is None:
+        t = _PINNED[nbytes] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    L.check(L.lib().sosx_memcpy(t.data_ptr(), ptr, nbytes, None), "sosx_memcpy")
+    return t.numpy()
+
+
+def direct(ptr, nbytes):
+    """Host copy of device memory by ONE D2H copy (no intermediate device buffer)."""
+    h = np.empty(nbytes, np.uint8)
+    L.check(L.lib().sosx_memcpy(h.ctypes.data, ptr, nbytes, None), "sosx_memcpy")
+    return h
 
 
 def runs_of(idx, k=4):
@@ -64,6 +85,7 @@ def main():
     n, n2 = a.n, a.n2
     hsrc = S.shmemx_malloc_device(n * 4)
     hdst = S.shmemx_malloc_device(n * 4)
+    hexp = S.shmemx_malloc_device(n * 4)
     fn = S.shmem_float_sum_reduce
     prev = None      # every PE's hsrc contents before this iteration's fill
     bad, checks = [], 0
@@ -78,7 +100,7 @@ def main():
             fn(world, hdst, hsrc, n2)
             e1 = O.recdbl(op, dt, [O.fill(dt, 0, seed + 3, q, n2) for q in range(P)])[me]
             checks += 1
-            m1 = int(np.count_nonzero(download(hdst, n2 * 4).view(np.uint32) != e1.view(np.uint32)))
+            m1 = int(np.count_nonzero(direct(hdst, n2 * 4).view(np.uint32) != e1.view(np.uint32)))
             if m1:
                 bad.append({"iter": it, "mode": "small_first", "mismatches": m1})
             grows += 1
@@ -86,31 +108,46 @@ def main():
             print(f"[p2p_stress] iteration {it}/{a.iters}", file=sys.stderr, flush=True)
         ins = [O.fill(dt, 0, seed, q, n) for q in range(P)]
         exp = O.recdbl(op, dt, ins)[me]
+        # the expected bytes in device memory for the kernel reader, checked after upload
+        L.check(L.lib().sosx_memcpy(hexp, exp.ctypes.data, n * 4, None), "sosx_memcpy")
+        assert np.array_equal(direct_pinned(hexp, n * 4), exp.view(np.uint8)), "expected-bytes upload"
         for mode in ("heap", "heap_inplace"):
             L.fill(dt, 0, seed, me, hsrc, n)
             torch.cuda.synchronize()
             out = hdst if mode == "heap" else hsrc
+            # what `out` held before this call: heap -> the small call's result in front of
+            # the previous iteration's result; in place -> this PE's own input
+            if mode == "heap":
+                before = prev.copy() if prev is not None else np.zeros(n, np.float32)
+                if a.release:
+                    before[:n2] = e1
+            else:
+                before = ins[me]
             fn(world, out, hsrc, n)
-            got = download(out, n * 4).view(np.float32)
+            # three readers of `out`, in this order: a D2H copy into pinned host memory (one
+            # DMA read of HBM), a D2H copy into pageable memory (staged by the runtime), and
+            # a kernel comparing `out` with the expected bytes uploaded (and read back) before
+            # the call (L2-coherent device reads)
+            seen = {"pinned": direct_pinned(out, n * 4).view(np.float32).copy(),
+                    "pageable": direct(out, n * 4).view(np.float32)}
+            kern = L.count_mismatch(hexp, out, n, 4)
             checks += 1
-            diff = np.nonzero(got.view(np.uint32) != exp.view(np.uint32))[0]
-            if diff.size:
-                torch.cuda.synchronize()
-                again = np.count_nonzero(download(out, n * 4).view(np.uint32) != exp.view(np.uint32))
-                culprits = []
-                if prev is not None:
-                    for q in range(P):
-                        if q == me:
-                            continue
-                        alt = [x[diff].copy() for x in ins]
-                        alt[q] = prev[diff].copy()
-                        if np.array_equal(O.recdbl(op, dt, alt)[me].view(np.uint32),
-                                          got[diff].view(np.uint32)):
-                            culprits.append(q)
-                bad.append({"iter": it, "mode": mode, "mismatches": int(diff.size),
-                            "runs": runs_of(diff), "recount": int(again),
-                            "stale_peer_explains": culprits,
-                            "sample": [(int(i), float(got[i]), float(exp[i])) for i in diff[:3]]})
+            dd = {how: np.nonzero(seen[how].view(np.uint32) != exp.view(np.uint32))[0] for how in seen}
+            if kern or any(v.size for v in dd.values()):
+                time.sleep(0.05)
+                later = direct_pinned(out, n * 4).view(np.uint32)
+                again = int(np.count_nonzero(later != exp.view(np.uint32)))
+                rec = {"iter": it, "mode": mode, "kernel_count": int(kern), "pinned_after_50ms": again}
+                for how in seen:
+                    diff = dd[how]
+                    if not diff.size:
+                        rec[how] = 0
+                        continue
+                    got = seen[how]
+                    stale = int(np.count_nonzero(got[diff].view(np.uint32) == before[diff].view(np.uint32)))
+                    rec[how] = {"mismatches": int(diff.size), "runs": runs_of(diff),
+                                "equal_to_previous_contents": stale}
+                bad.append(rec)
         prev = exp  # hsrc now holds the in-place result on every PE (same value everywhere)
         # a staged call through the stage region, as team_check's "device" mode
         t_in = torch.empty(n2 * 4, dtype=torch.uint8, device="cuda")
@@ -125,11 +162,12 @@ def main():
         if m2:
             bad.append({"iter": it, "mode": "device_staged", "mismatches": m2})
     S.shmem_barrier_all()
+    S.shmemx_free_device(hexp)
     S.shmemx_free_device(hdst)
     S.shmemx_free_device(hsrc)
     S.shmem_finalize()
     if bad:
-        print(f"PE {me}/{P}: {len(bad)} of {checks} FAILED: {bad[:4]}", flush=True)
+        print(f"PE {me}/{P}: {len(bad)} of {checks} FAILED: {bad[:6]}", flush=True)
         return 1
     print(f"PE {me}/{P}: {checks} checks OK ({a.alg}, n={n}, {a.iters} iterations, "
           f"{grows} calls right after a scratch grow)", flush=True)
