@@ -144,6 +144,21 @@ void stall_hook()
 #endif
 }
 
+// Completion of a round's sends / of the call: sync_system (runtime.h).  Test build only:
+// SOSX_TEST_PLAIN_SYNC=1 restores round 4's plain hipStreamSynchronize, for the A/B of
+// tools/p2p_stress.py.
+hipError_t complete(hipStream_t stream)
+{
+#ifdef SOSX_TEST_HOOKS
+    static const bool plain = [] {
+        const char *e = getenv("SOSX_TEST_PLAIN_SYNC");
+        return e && *e == '1';
+    }();
+    if (plain) return hipStreamSynchronize(stream);
+#endif
+    return sync_system(stream);
+}
+
 double wait_limit_s()
 {
     static const double lim = [] {
@@ -697,7 +712,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
         if (any_send) {
             // the sent bytes must be in HBM, not only complete: peers on other GPUs read
             // them over xGMI, which no L2 of this GPU serves (system-scope release)
-            if (sync_system(stream) != hipSuccess) return SOSX_ERR_HIP;
+            if (complete(stream) != hipSuccess) return SOSX_ERR_HIP;
             phase(PH_SYNC_SEND);
             for (const auto &x : r.xfers)
                 if (x.send) {
@@ -782,7 +797,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
             if (rc) return rc;
         }
     }
-    const hipError_t e = sync_system(stream);  // the caller's result in HBM (sync_system)
+    const hipError_t e = complete(stream);  // the caller's result in HBM (sync_system)
     phase(PH_SYNC_END);
     if (tr && ++g_trace.calls % g_trace.every == 0) {  // window averages, then reset
         const double k = 1e6 / (double)g_trace.every;

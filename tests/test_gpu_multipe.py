@@ -243,8 +243,8 @@ def test_device_heap_colours():
     colours (consecutive ones an odd multiple of 4 KiB apart), at the same offsets on
     every PE (symmetric)."""
     r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "heap_colour_pe.py")], timeout=120,
-               extra_env={"SHMEMX_DEVICE_HEAP_SIZE": "1G", "SHMEMX_STAGE_BYTES": "512M",
-                          "HEAP_REGION_BYTES": str(512 << 20)})
+               extra_env={"SHMEMX_DEVICE_HEAP_SIZE": "1G", "SHMEMX_STAGE_BYTES": "64M",
+                          "HEAP_REGION_BYTES": str(960 << 20)})
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     # PEs print concurrently: match the reports, not lines
     lines = re.findall(r"PE \d: (colours \[[\d, ]+\] offsets \[[\d, ]+\])", r.stdout)

@@ -75,6 +75,9 @@ def main():
                     help="every iteration starts from released workspaces and runs a small call "
                          "first, so each big call is the first after its scratch grew (hipFree + "
                          "hipMalloc), the condition of the round-4 failure, every iteration")
+    ap.add_argument("--reader", default="three", choices=("three", "download"),
+                    help="three: pinned D2H, pageable D2H and a compare kernel; download: round "
+                         "4's path only (D2D into a torch buffer, then torch's D2H)")
     a = ap.parse_args()
     S.shmem_init()
     me, P = S.shmem_my_pe(), S.shmem_n_pes()
@@ -128,9 +131,13 @@ def main():
             # DMA read of HBM), a D2H copy into pageable memory (staged by the runtime), and
             # a kernel comparing `out` with the expected bytes uploaded (and read back) before
             # the call (L2-coherent device reads)
-            seen = {"pinned": direct_pinned(out, n * 4).view(np.float32).copy(),
-                    "pageable": direct(out, n * 4).view(np.float32)}
-            kern = L.count_mismatch(hexp, out, n, 4)
+            if a.reader == "download":
+                seen = {"download": download(out, n * 4).view(np.float32)}
+                kern = 0
+            else:
+                seen = {"pinned": direct_pinned(out, n * 4).view(np.float32).copy(),
+                        "pageable": direct(out, n * 4).view(np.float32)}
+                kern = L.count_mismatch(hexp, out, n, 4)
             checks += 1
             dd = {how: np.nonzero(seen[how].view(np.uint32) != exp.view(np.uint32))[0] for how in seen}
             if kern or any(v.size for v in dd.values()):
