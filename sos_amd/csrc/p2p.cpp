@@ -47,6 +47,7 @@
 #include <tuple>
 #include <vector>
 
+#include "p2p_proto.h"
 #include "plan.h"
 #include "runtime.h"
 #include "sosx.h"
@@ -62,41 +63,13 @@ void prof_mark(int which, bool end, hipStream_t s);  // collectives.cpp (0 = fol
 
 namespace {
 
-constexpr int kMaxPE = 64;
+using sosp2p::kMaxPE;
+using sosp2p::kDescRing;
+using sosp2p::Desc;
+using P2PShared = sosp2p::Shared;
+using sosp2p::round_fusable;
 
-constexpr int kDescRing = 4;
-
-// Per-call buffer offsets of a sender, as the receiver needs them to find its bytes.
-struct Desc {
-    uint64_t src_off, dst_off, scr_off, mis;
-};
-
-struct P2PShared {
-    std::atomic<uint64_t> posted[kMaxPE][kMaxPE];
-    std::atomic<uint64_t> consumed[kMaxPE][kMaxPE];
-    // stream mode: counters stored by the GPUs (sosx_p2p_signal), cumulative per pair
-    uint64_t dposted[kMaxPE][kMaxPE];
-    uint64_t dconsumed[kMaxPE][kMaxPE];
-    uint64_t sig_err[kMaxPE];                  // a PE's timed-out device wait
-    // stream mode: descriptor ring per ordered pair [from][to]
-    Desc desc[kMaxPE][kMaxPE][kDescRing];
-    std::atomic<uint64_t> desc_posted[kMaxPE][kMaxPE];
-    std::atomic<uint64_t> desc_read[kMaxPE][kMaxPE];
-    struct Pub {
-        std::atomic<uint64_t> src_off, dst_off, scr_off, mis;
-    } pub[kMaxPE];
-    // team creation agreement (runtime.cpp shmem_team_split_strided): per world PE, the
-    // free team-slot bit mask and the creation status, read by the other members
-    std::atomic<uint64_t> team_word[2][kMaxPE];
-};
-
-// What this PE has seen/done per ordered pair (monotonic across calls).
-struct Local {
-    uint64_t posted_by_me[kMaxPE] = {0};      // posts I made to each peer
-    uint64_t seen_from[kMaxPE] = {0};         // posts from each peer I have consumed
-};
-
-Local g_local;
+sosp2p::Local g_local;
 
 // stream-mode signalling state
 struct Sig {
@@ -234,35 +207,14 @@ bool trace_on()
     return g_trace.every > 0;
 }
 
-struct PeerSend {
-    int buf;
-    uint64_t off, bytes;
-};
-
-// The sends peer q's plan makes to `me`, in order (deterministic: rebuild q's plan from
-// its published operand misalignment, which places its scratch slots).
-const std::vector<PeerSend> &peer_sends(int alg, int P, int q, int me, uint64_t count,
-                                        uint64_t ts, uint64_t mis)
+// The sends peer q's plan makes to `me`, in order (p2p_proto.h), or the end of the job.
+const std::vector<sosp2p::PeerSend> &peer_sends(int alg, int P, int q, int me, uint64_t count,
+                                                uint64_t ts, uint64_t mis)
 {
-    static std::map<std::tuple<int, int, int, int, uint64_t, uint64_t, uint64_t>,
-                    std::vector<PeerSend>> cache;
-    auto key = std::make_tuple(alg, P, q, me, count, ts, mis);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    if (cache.size() > 512) cache.clear();
-    sosplan::Plan p;
-    if (sosplan::build(alg, P, q, count, ts, (unsigned)(mis & 15), (unsigned)(mis >> 4), &p) != SOSX_OK)
-        raise_error("p2p transport: cannot build the plan of PE %d", q);
-    std::vector<PeerSend> v;
-    for (const auto &r : p.rounds)
-        for (const auto &x : r.xfers)
-            if (x.send && x.peer == me) v.push_back(PeerSend{x.buf, x.off, x.bytes});
-    return cache.emplace(key, std::move(v)).first->second;
-}
-
-bool overlaps(const char *a, uint64_t na, const char *b, uint64_t nb)
-{
-    return a < b + nb && b < a + na;
+    bool ok;
+    const auto &v = sosp2p::peer_sends(alg, P, q, me, count, ts, mis, &ok);
+    if (!ok) raise_error("p2p transport: cannot build the plan of PE %d", q);
+    return v;
 }
 
 }  // namespace
@@ -317,26 +269,6 @@ int run_round_ops(const sosplan::Round &r, const std::vector<std::vector<const v
         if (rc) return rc;
     }
     return SOSX_OK;
-}
-
-// Does any output of the round's ops overlap bytes this PE sends in the same round?
-// If not, folds/prefixes may read received chunks in place (the peers' memory) before
-// the round's sends are consumed.
-bool round_fusable(const sosplan::Round &r, uint64_t ts,
-                   const std::function<char *(int, uint64_t)> &local_ptr)
-{
-    for (const auto &l : r.ops) {
-        const bool typed = l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX;
-        const uint64_t ob = typed ? l.count * ts : l.count;
-        const int nout = l.kind == sosplan::PREFIX ? l.nout : 1;
-        for (int k = 0; k < nout; ++k) {
-            const char *o = l.kind == sosplan::PREFIX ? local_ptr(l.outs_buf[k], l.outs_off[k])
-                                                      : local_ptr(l.out_buf, l.out_off);
-            for (const auto &x : r.xfers)
-                if (x.send && overlaps(o, ob, local_ptr(x.buf, x.off), x.bytes)) return false;
-        }
-    }
-    return true;
 }
 
 // Stream-mode executor: the whole call is enqueued at once (see the header).
@@ -467,7 +399,7 @@ int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t 
             const int k = recv_idx[(size_t)x.peer]++;
             if (k >= (int)sends.size() || sends[(size_t)k].bytes != x.bytes)
                 raise_error("p2p transport: plan mismatch with PE %d", pw);
-            const PeerSend &ps = sends[(size_t)k];
+            const sosp2p::PeerSend &ps = sends[(size_t)k];
             const uint64_t boff = ps.buf == sosplan::SRC ? d.src_off
                                 : ps.buf == sosplan::DST ? d.dst_off : d.scr_off;
             segs.push_back(Seg{s.peer_heap[(size_t)pw] + boff + ps.off, local_ptr(x.buf, x.off),
@@ -586,7 +518,7 @@ void p2p_signal_setup()
     const bool reg = g_sig.registered;
     g_sig = Sig();
     g_sig.registered = reg;
-    g_local = Local();
+    g_local = sosp2p::Local();
     if (!s.shm.extra || s.n_pes <= 1) return;
     int ok = 1;
     void *dptr = nullptr;
@@ -679,6 +611,42 @@ extern "C" int sosx_set_p2p_signal_mode(int mode)
 
 namespace sosrt {
 
+namespace {
+
+// The host-signalling protocol's backend on this PE's HIP stream (p2p_proto.h).
+struct HipBackend {
+    hipStream_t stream;
+    int op, dt;
+    double tp;
+    bool tr;
+    int complete() { return sosrt::complete(stream) == hipSuccess ? 0 : 1; }
+    int drain() { return hipStreamSynchronize(stream) == hipSuccess ? 0 : 1; }
+    int gather(int n, const void *const *srcs, void *const *dsts, const size_t *bytes)
+    {
+        prof_mark(1, false, stream);
+        const int rc = sosx_gather(n, srcs, dsts, bytes, stream);
+        prof_mark(1, true, stream);
+        return rc;
+    }
+    int run_ops(const sosplan::Round &r, const std::vector<std::vector<const void *>> &ins,
+                const sosp2p::LocalPtr &local_ptr)
+    {
+        return run_round_ops(r, ins, local_ptr, op, dt, stream);
+    }
+    const char *peer_base(int pw) { return st().peer_heap[(size_t)pw]; }
+    void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what) { spin_until(a, want, what); }
+    void plan_mismatch(int pw) { raise_error("p2p transport: plan mismatch with PE %d", pw); }
+    void phase(int ph)
+    {
+        if (!tr) return;
+        const double now = now_s();
+        g_trace.t[ph] += now - tp;
+        tp = now;
+    }
+};
+
+}  // namespace
+
 int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, uint64_t ts,
              const P2PBufs &b, int op, int dt, hipStream_t stream)
 {
@@ -686,119 +654,11 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
     P2PShared *sh = shared();
     if (!sh) return SOSX_ERR_STATE;
     if (g_sig.on) return p2p_exec_stream(plan, t, alg, count, ts, b, op, dt, stream);
-    const int me = t.my_idx;
-    const int my_world = t.world_rank(me);
-    sh->pub[my_world].src_off.store(b.src_off, std::memory_order_relaxed);
-    sh->pub[my_world].scr_off.store(b.scr_off, std::memory_order_relaxed);
-    sh->pub[my_world].mis.store((uint64_t)(b.smis & 15) | (uint64_t)(b.dmis & 15) << 4,
-                                std::memory_order_relaxed);
-    sh->pub[my_world].dst_off.store(b.dst_off, std::memory_order_release);
-    std::vector<int> recv_idx((size_t)t.size, 0);  // k-th receive from each team peer
     const bool tr = trace_on();
-    double tp = tr ? now_s() : 0;
-    auto phase = [&](int ph) {
-        if (!tr) return;
-        const double now = now_s();
-        g_trace.t[ph] += now - tp;
-        tp = now;
-    };
-    std::function<char *(int, uint64_t)> local_ptr = [&](int buf, uint64_t off) -> char * {
-        return (buf == sosplan::SRC ? (char *)b.src : buf == sosplan::DST ? b.dst : b.scr) + off;
-    };
-    for (const auto &r : plan.rounds) {
-        // 1. post sends
-        bool any_send = false;
-        for (const auto &x : r.xfers) any_send |= x.send != 0;
-        if (any_send) {
-            // the sent bytes must be in HBM, not only complete: peers on other GPUs read
-            // them over xGMI, which no L2 of this GPU serves (system-scope release)
-            if (complete(stream) != hipSuccess) return SOSX_ERR_HIP;
-            phase(PH_SYNC_SEND);
-            for (const auto &x : r.xfers)
-                if (x.send) {
-                    const int pw = t.world_rank(x.peer);
-                    sh->posted[my_world][pw].fetch_add(1, std::memory_order_release);
-                    g_local.posted_by_me[pw]++;
-                }
-        }
-        // 2. locate every receive in the sender's memory
-        struct Seg { const char *src; char *dst; uint64_t bytes; int peer_world; bool used; };
-        std::vector<Seg> segs;
-        for (const auto &x : r.xfers) {
-            if (x.send) continue;
-            const int pw = t.world_rank(x.peer);
-            const uint64_t want = ++g_local.seen_from[pw];
-            spin_until(sh->posted[pw][my_world], want, "a peer's data");
-            phase(PH_WAIT_POST);
-            const uint64_t dst_off = sh->pub[pw].dst_off.load(std::memory_order_acquire);
-            const auto &sends = peer_sends(alg, t.size, x.peer, me, count, ts,
-                                           sh->pub[pw].mis.load(std::memory_order_relaxed));
-            const int k = recv_idx[(size_t)x.peer]++;
-            if (k >= (int)sends.size() || sends[(size_t)k].bytes != x.bytes)
-                raise_error("p2p transport: plan mismatch with PE %d", pw);
-            const PeerSend &ps = sends[(size_t)k];
-            const uint64_t boff = ps.buf == sosplan::SRC ? sh->pub[pw].src_off.load(std::memory_order_relaxed)
-                                : ps.buf == sosplan::DST ? dst_off
-                                                         : sh->pub[pw].scr_off.load(std::memory_order_relaxed);
-            const char *remote = s.peer_heap[(size_t)pw] + boff + ps.off;
-            segs.push_back(Seg{remote, local_ptr(x.buf, x.off), x.bytes, pw, false});
-        }
-        // 3. folds/prefixes read received chunks in place when no output overlaps a send
-        const bool fuse_ok = round_fusable(r, ts, local_ptr);
-        std::vector<std::vector<const void *>> fold_ins(r.ops.size());
-        for (size_t i = 0; i < r.ops.size(); ++i) {
-            const auto &l = r.ops[i];
-            for (int k = 0; k < l.nin; ++k) {
-                const char *p = local_ptr(l.in_buf[k], l.in_off[k]);
-                if (fuse_ok && (l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX))
-                    for (auto &sg : segs)
-                        if (sg.dst == p && sg.bytes == l.count * ts) {
-                            p = sg.src;
-                            sg.used = true;
-                        }
-                fold_ins[i].push_back(p);
-            }
-        }
-        std::vector<const void *> gs;
-        std::vector<void *> gd;
-        std::vector<size_t> gb;
-        for (auto &sg : segs)
-            if (!sg.used) {
-                gs.push_back(sg.src);
-                gd.push_back(sg.dst);
-                gb.push_back(sg.bytes);
-            }
-        if (!gs.empty()) {
-            prof_mark(1, false, stream);
-            int rc = sosx_gather((int)gs.size(), gs.data(), gd.data(), gb.data(), stream);
-            prof_mark(1, true, stream);
-            if (rc) return rc;
-        }
-        auto run_ops = [&]() { return run_round_ops(r, fold_ins, local_ptr, op, dt, stream); };
-        if (fuse_ok) {
-            int rc = run_ops();
-            if (rc) return rc;
-        }
-        // 4. receives done -> consumed; wait for my sends to be consumed
-        phase(PH_ENQUEUE);
-        if (!segs.empty() || fuse_ok) {
-            if (hipStreamSynchronize(stream) != hipSuccess) return SOSX_ERR_HIP;
-        }
-        phase(PH_SYNC_OPS);
-        for (auto &sg : segs) sh->consumed[sg.peer_world][my_world].fetch_add(1, std::memory_order_release);
-        for (const auto &x : r.xfers)
-            if (x.send) {
-                const int pw = t.world_rank(x.peer);
-                spin_until(sh->consumed[my_world][pw], g_local.posted_by_me[pw], "a peer to read");
-            }
-        phase(PH_WAIT_CONSUMED);
-        if (!fuse_ok) {
-            int rc = run_ops();
-            if (rc) return rc;
-        }
-    }
-    const hipError_t e = complete(stream);  // the caller's result in HBM (sync_system)
-    phase(PH_SYNC_END);
+    HipBackend be{stream, op, dt, tr ? now_s() : 0, tr};
+    const sosp2p::Bufs pb{b.src, b.dst, b.scr, b.src_off, b.dst_off, b.scr_off, b.smis, b.dmis};
+    const int rc = sosp2p::exec_host(plan, t.size, t.my_idx, [&](int i) { return t.world_rank(i); }, alg,
+                                     count, ts, pb, sh, g_local, be);
     if (tr && ++g_trace.calls % g_trace.every == 0) {  // window averages, then reset
         const double k = 1e6 / (double)g_trace.every;
         fprintf(stderr, "[%04d] p2p trace (calls %ld-%ld, us/call): sync-send %.1f wait-post %.1f "
@@ -807,7 +667,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
                 g_trace.t[2] * k, g_trace.t[3] * k, g_trace.t[4] * k, g_trace.t[5] * k);
         for (double &v : g_trace.t) v = 0;
     }
-    return e == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
+    return rc;
 }
 
 }  // namespace sosrt

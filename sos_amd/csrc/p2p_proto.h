@@ -1,0 +1,247 @@
+// p2p_proto.h -- the peer-to-peer transport's pairing protocol in host-signalling mode,
+// written once over a backend: p2p.cpp instantiates it with the HIP stream (kernels,
+// system-scope completion), tests/p2p_proto_harness.cpp with CPU threads and memcpy
+// (run under ThreadSanitizer: every byte a PE reads from a peer must be ordered after the
+// peer's writes by the protocol's release/acquire counters, and every overwrite after
+// the peers' reads).
+//
+// The protocol (see p2p.cpp's header): a transfer is a PULL.  Per round, at PE me:
+//   1. if the round sends: complete the stream (the sent bytes are final and in memory),
+//      then post every send (posted[me][to]++ , release);
+//   2. for every receive: wait for the peer's post (acquire), locate the bytes from the
+//      peer's plan (deterministic) and its published offsets;
+//   3. folds/prefixes read received chunks in place when no output of the round
+//      overlaps what this PE sends in it; the other receives are gathered by one copy;
+//   4. complete the stream, mark every receive consumed (consumed[from][me]++, release),
+//      wait until every peer consumed this PE's sends (acquire); then the round's
+//      remaining (non-fused) ops.
+// Only headers that need no HIP: plan.h (the plans) and <atomic>.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include <atomic>
+#include <functional>
+#include <map>
+#include <tuple>
+#include <vector>
+
+#include "plan.h"
+
+namespace sosp2p {
+
+constexpr int kMaxPE = 64;
+constexpr int kDescRing = 4;
+
+// Per-call buffer offsets of a sender, as the receiver needs them to find its bytes.
+struct Desc {
+    uint64_t src_off, dst_off, scr_off, mis;
+};
+
+// The node-shared segment of the transport (one per job, every PE maps it).
+struct Shared {
+    std::atomic<uint64_t> posted[kMaxPE][kMaxPE];
+    std::atomic<uint64_t> consumed[kMaxPE][kMaxPE];
+    // stream mode: counters stored by the GPUs (sosx_p2p_signal), cumulative per pair
+    uint64_t dposted[kMaxPE][kMaxPE];
+    uint64_t dconsumed[kMaxPE][kMaxPE];
+    uint64_t sig_err[kMaxPE];                  // a PE's timed-out device wait
+    // stream mode: descriptor ring per ordered pair [from][to]
+    Desc desc[kMaxPE][kMaxPE][kDescRing];
+    std::atomic<uint64_t> desc_posted[kMaxPE][kMaxPE];
+    std::atomic<uint64_t> desc_read[kMaxPE][kMaxPE];
+    struct Pub {
+        std::atomic<uint64_t> src_off, dst_off, scr_off, mis;
+    } pub[kMaxPE];
+    // team creation agreement (runtime.cpp shmem_team_split_strided): per world PE, the
+    // free team-slot bit mask and the creation status, read by the other members
+    std::atomic<uint64_t> team_word[2][kMaxPE];
+};
+
+// What one PE has seen/done per ordered pair (monotonic across calls).
+struct Local {
+    uint64_t posted_by_me[kMaxPE] = {0};      // posts I made to each peer
+    uint64_t seen_from[kMaxPE] = {0};         // posts from each peer I have consumed
+};
+
+// One call's buffers at this PE: addresses, and the heap offsets the peers rebuild them from.
+struct Bufs {
+    const char *src;
+    char *dst;
+    char *scr;
+    uint64_t src_off, dst_off, scr_off;
+    unsigned smis, dmis;      // src/dst address mod 16 the plan was built with
+};
+
+struct PeerSend {
+    int buf;
+    uint64_t off, bytes;
+};
+
+// The sends peer q's plan makes to `me`, in order (deterministic: rebuild q's plan from
+// its published operand misalignment, which places its scratch slots).  Empty with
+// *ok = false when q's plan cannot be built.
+inline const std::vector<PeerSend> &peer_sends(int alg, int P, int q, int me, uint64_t count,
+                                               uint64_t ts, uint64_t mis, bool *ok)
+{
+    static thread_local std::map<std::tuple<int, int, int, int, uint64_t, uint64_t, uint64_t>,
+                                 std::vector<PeerSend>> cache;
+    *ok = true;
+    auto key = std::make_tuple(alg, P, q, me, count, ts, mis);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    if (cache.size() > 512) cache.clear();
+    sosplan::Plan p;
+    std::vector<PeerSend> v;
+    if (sosplan::build(alg, P, q, count, ts, (unsigned)(mis & 15), (unsigned)(mis >> 4), &p) != SOSX_OK) {
+        *ok = false;
+        static thread_local std::vector<PeerSend> none;
+        return none;
+    }
+    for (const auto &r : p.rounds)
+        for (const auto &x : r.xfers)
+            if (x.send && x.peer == me) v.push_back(PeerSend{x.buf, x.off, x.bytes});
+    return cache.emplace(key, std::move(v)).first->second;
+}
+
+inline bool overlaps(const char *a, uint64_t na, const char *b, uint64_t nb)
+{
+    return a < b + nb && b < a + na;
+}
+
+using LocalPtr = std::function<char *(int, uint64_t)>;
+
+// Does any output of the round's ops overlap bytes this PE sends in the same round?
+// If not, folds/prefixes may read received chunks in place (the peers' memory) before
+// the round's sends are consumed.
+inline bool round_fusable(const sosplan::Round &r, uint64_t ts, const LocalPtr &local_ptr)
+{
+    for (const auto &l : r.ops) {
+        const bool typed = l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX;
+        const uint64_t ob = typed ? l.count * ts : l.count;
+        const int nout = l.kind == sosplan::PREFIX ? l.nout : 1;
+        for (int k = 0; k < nout; ++k) {
+            const char *o = l.kind == sosplan::PREFIX ? local_ptr(l.outs_buf[k], l.outs_off[k])
+                                                      : local_ptr(l.out_buf, l.out_off);
+            for (const auto &x : r.xfers)
+                if (x.send && overlaps(o, ob, local_ptr(x.buf, x.off), x.bytes)) return false;
+        }
+    }
+    return true;
+}
+
+// Host-signalled executor of one plan at team index `me` of a team whose team index i is
+// world PE world_of(i).  Backend B provides (all on this PE's ordered "stream"):
+//   int complete()        drain the stream, stores in memory (system scope); 0 = ok
+//   int drain()           drain the stream (this PE's reads are done); 0 = ok
+//   int gather(n, srcs, dsts, bytes)                      one multi-segment copy
+//   int run_ops(round, ins, local_ptr)                    the round's local ops
+//   const char *peer_base(world_pe)                       the peer's heap, mapped here
+//   void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what)   bounded wait
+//   void plan_mismatch(world_pe)                          fatal
+//   void phase(int)                                        tracing (may be a no-op)
+template <class B, class WorldOf>
+int exec_host(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of, int alg,
+              uint64_t count, uint64_t ts, const Bufs &b, Shared *sh, Local &loc, B &be)
+{
+    enum { PH_SYNC_SEND, PH_WAIT_POST, PH_ENQUEUE, PH_SYNC_OPS, PH_WAIT_CONSUMED, PH_SYNC_END };
+    const int my_world = world_of(me);
+    sh->pub[my_world].src_off.store(b.src_off, std::memory_order_relaxed);
+    sh->pub[my_world].scr_off.store(b.scr_off, std::memory_order_relaxed);
+    sh->pub[my_world].mis.store((uint64_t)(b.smis & 15) | (uint64_t)(b.dmis & 15) << 4,
+                                std::memory_order_relaxed);
+    sh->pub[my_world].dst_off.store(b.dst_off, std::memory_order_release);
+    std::vector<int> recv_idx((size_t)P, 0);  // k-th receive from each team peer
+    LocalPtr local_ptr = [&](int buf, uint64_t off) -> char * {
+        return (buf == sosplan::SRC ? (char *)b.src : buf == sosplan::DST ? b.dst : b.scr) + off;
+    };
+    for (const auto &r : plan.rounds) {
+        // 1. post sends, once their bytes are final and in memory
+        bool any_send = false;
+        for (const auto &x : r.xfers) any_send |= x.send != 0;
+        if (any_send) {
+            if (be.complete() != 0) return SOSX_ERR_HIP;
+            be.phase(PH_SYNC_SEND);
+            for (const auto &x : r.xfers)
+                if (x.send) {
+                    const int pw = world_of(x.peer);
+                    sh->posted[my_world][pw].fetch_add(1, std::memory_order_release);
+                    loc.posted_by_me[pw]++;
+                }
+        }
+        // 2. locate every receive in the sender's memory
+        struct Seg { const char *src; char *dst; uint64_t bytes; int peer_world; bool used; };
+        std::vector<Seg> segs;
+        for (const auto &x : r.xfers) {
+            if (x.send) continue;
+            const int pw = world_of(x.peer);
+            const uint64_t want = ++loc.seen_from[pw];
+            be.spin(sh->posted[pw][my_world], want, "a peer's data");
+            be.phase(PH_WAIT_POST);
+            const uint64_t dst_off = sh->pub[pw].dst_off.load(std::memory_order_acquire);
+            bool ok;
+            const auto &sends = peer_sends(alg, P, x.peer, me, count, ts,
+                                           sh->pub[pw].mis.load(std::memory_order_relaxed), &ok);
+            const int k = recv_idx[(size_t)x.peer]++;
+            if (!ok || k >= (int)sends.size() || sends[(size_t)k].bytes != x.bytes) be.plan_mismatch(pw);
+            const PeerSend &ps = sends[(size_t)k];
+            const uint64_t boff = ps.buf == sosplan::SRC ? sh->pub[pw].src_off.load(std::memory_order_relaxed)
+                                : ps.buf == sosplan::DST ? dst_off
+                                                         : sh->pub[pw].scr_off.load(std::memory_order_relaxed);
+            segs.push_back(Seg{be.peer_base(pw) + boff + ps.off, local_ptr(x.buf, x.off), x.bytes, pw, false});
+        }
+        // 3. folds/prefixes read received chunks in place when no output overlaps a send
+        const bool fuse_ok = round_fusable(r, ts, local_ptr);
+        std::vector<std::vector<const void *>> ins(r.ops.size());
+        for (size_t i = 0; i < r.ops.size(); ++i) {
+            const auto &l = r.ops[i];
+            for (int k = 0; k < l.nin; ++k) {
+                const char *p = local_ptr(l.in_buf[k], l.in_off[k]);
+                if (fuse_ok && (l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX))
+                    for (auto &sg : segs)
+                        if (sg.dst == p && sg.bytes == l.count * ts) {
+                            p = sg.src;
+                            sg.used = true;
+                        }
+                ins[i].push_back(p);
+            }
+        }
+        std::vector<const void *> gs;
+        std::vector<void *> gd;
+        std::vector<size_t> gb;
+        for (auto &sg : segs)
+            if (!sg.used) {
+                gs.push_back(sg.src);
+                gd.push_back(sg.dst);
+                gb.push_back(sg.bytes);
+            }
+        if (!gs.empty()) {
+            const int rc = be.gather((int)gs.size(), gs.data(), gd.data(), gb.data());
+            if (rc) return rc;
+        }
+        if (fuse_ok) {
+            const int rc = be.run_ops(r, ins, local_ptr);
+            if (rc) return rc;
+        }
+        // 4. receives done -> consumed; wait for my sends to be consumed
+        be.phase(PH_ENQUEUE);
+        if ((!segs.empty() || fuse_ok) && be.drain() != 0) return SOSX_ERR_HIP;
+        be.phase(PH_SYNC_OPS);
+        for (auto &sg : segs) sh->consumed[sg.peer_world][my_world].fetch_add(1, std::memory_order_release);
+        for (const auto &x : r.xfers)
+            if (x.send) {
+                const int pw = world_of(x.peer);
+                be.spin(sh->consumed[my_world][pw], loc.posted_by_me[pw], "a peer to read");
+            }
+        be.phase(PH_WAIT_CONSUMED);
+        if (!fuse_ok) {
+            const int rc = be.run_ops(r, ins, local_ptr);
+            if (rc) return rc;
+        }
+    }
+    const int e = be.complete();  // the caller's result in memory
+    be.phase(PH_SYNC_END);
+    return e == 0 ? SOSX_OK : SOSX_ERR_HIP;
+}
+
+}  // namespace sosp2p

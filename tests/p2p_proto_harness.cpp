@@ -1,0 +1,291 @@
+// p2p_proto_harness.cpp -- the p2p transport's host-signalling protocol (the product's own
+// sosp2p::exec_host, sos_amd/csrc/p2p_proto.h) on CPU threads, for ThreadSanitizer.
+//
+// Test infrastructure (tests/test_p2p_proto.py builds and runs it; no GPU).  Each PE is a
+// host thread with a "stream": a worker thread that runs the PE's queued copies and folds
+// in order, as the GPU runs its stream.  Each PE's device heap is a host buffer every
+// thread can read (the IPC mapping); the node-shared counters are sosp2p::Shared.  The
+// plans are the product's (plan.cpp), the arithmetic is uint32 wrapping addition (order-
+// independent, so every schedule's result is the plain sum / prefix / root's bytes).
+// Every call's result is checked; under -fsanitize=thread every byte a worker reads from
+// a peer must be ordered after the peer's writes, and every overwrite after the peers'
+// reads, by the protocol's counters alone.
+//
+// Build with -DBROKEN_DRAIN to drop the drain before a round's receives are marked
+// consumed (step 4): the sanitizer must then report the race (the negative control).
+//
+// Usage: p2p_proto_harness [iters]     prints "p2p protocol harness: N calls OK", exit 0
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "p2p_proto.h"
+
+namespace {
+
+struct Stream {
+    std::mutex m;
+    std::condition_variable cv, idle;
+    std::deque<std::function<void()>> q;
+    bool stop = false;
+    int busy = 0;
+    std::thread th;
+    Stream()
+    {
+        th = std::thread([this] {
+            for (;;) {
+                std::function<void()> f;
+                {
+                    std::unique_lock<std::mutex> lk(m);
+                    cv.wait(lk, [&] { return stop || !q.empty(); });
+                    if (q.empty()) return;
+                    f = std::move(q.front());
+                    q.pop_front();
+                    busy = 1;
+                }
+                f();
+                {
+                    std::lock_guard<std::mutex> lk(m);
+                    busy = 0;
+                    if (q.empty()) idle.notify_all();
+                }
+            }
+        });
+    }
+    ~Stream()
+    {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
+    void push(std::function<void()> f)
+    {
+        std::lock_guard<std::mutex> lk(m);
+        q.push_back(std::move(f));
+        cv.notify_all();
+    }
+    void drain()
+    {
+        std::unique_lock<std::mutex> lk(m);
+        idle.wait(lk, [&] { return q.empty() && !busy; });
+    }
+};
+
+std::vector<char *> g_heaps;
+constexpr size_t kHeap = 8u << 20;
+
+[[noreturn]] void die(const char *what, int a = 0, int b = 0)
+{
+    fprintf(stderr, "p2p protocol harness: %s (%d %d)\n", what, a, b);
+    fflush(stderr);
+    abort();
+}
+
+struct CpuBackend {
+    Stream *s;
+    int complete()
+    {
+        s->drain();
+        return 0;
+    }
+    int drain()
+    {
+#ifndef BROKEN_DRAIN
+        s->drain();
+#endif
+        return 0;
+    }
+    int gather(int n, const void *const *srcs, void *const *dsts, const size_t *bytes)
+    {
+        std::vector<const void *> sv(srcs, srcs + n);
+        std::vector<void *> dv(dsts, dsts + n);
+        std::vector<size_t> bv(bytes, bytes + n);
+        s->push([sv, dv, bv] {
+            for (size_t i = 0; i < sv.size(); ++i) memcpy(dv[i], sv[i], bv[i]);
+        });
+        return 0;
+    }
+    int run_ops(const sosplan::Round &r, const std::vector<std::vector<const void *>> &ins,
+                const sosp2p::LocalPtr &local_ptr)
+    {
+        for (size_t i = 0; i < r.ops.size(); ++i) {
+            const sosplan::Local l = r.ops[i];
+            const std::vector<const void *> in = ins[i];
+            if (l.kind == sosplan::COPY) {
+                char *o = local_ptr(l.out_buf, l.out_off);
+                s->push([o, in, l] { if (o != in[0]) memmove(o, in[0], l.count); });
+            } else if (l.kind == sosplan::ZERO) {
+                char *o = local_ptr(l.out_buf, l.out_off);
+                s->push([o, l] { memset(o, 0, l.count); });
+            } else if (l.kind == sosplan::FOLD) {
+                char *o = local_ptr(l.out_buf, l.out_off);
+                s->push([o, in, l] {
+                    for (uint64_t e = 0; e < l.count; ++e) {
+                        uint32_t acc = 0, v;
+                        for (int k = 0; k < l.nin; ++k) {
+                            memcpy(&v, (const char *)in[(size_t)k] + 4 * e, 4);
+                            acc += v;
+                        }
+                        memcpy(o + 4 * e, &acc, 4);
+                    }
+                });
+            } else {  // PREFIX: every input of an element before the first store
+                std::vector<char *> outs;
+                for (int k = 0; k < l.nout; ++k) outs.push_back(local_ptr(l.outs_buf[k], l.outs_off[k]));
+                s->push([outs, in, l] {
+                    std::vector<uint32_t> v((size_t)l.nin);
+                    for (uint64_t e = 0; e < l.count; ++e) {
+                        for (int k = 0; k < l.nin; ++k) memcpy(&v[(size_t)k], (const char *)in[(size_t)k] + 4 * e, 4);
+                        uint32_t acc = 0;
+                        for (int k = 0; k < l.nin; ++k) {
+                            acc += v[(size_t)k];
+                            memcpy(outs[(size_t)k] + 4 * e, &acc, 4);
+                        }
+                    }
+                });
+            }
+        }
+        return 0;
+    }
+    const char *peer_base(int pw) { return g_heaps[(size_t)pw]; }
+    void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what)
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (a.load(std::memory_order_acquire) < want) {
+            std::this_thread::yield();
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) die(what);
+        }
+    }
+    void plan_mismatch(int pw) { die("plan mismatch", pw); }
+    void phase(int) {}
+};
+
+uint32_t val(uint64_t call, int pe, uint64_t i)
+{
+    uint64_t x = call * 0x9E3779B97F4A7C15ull ^ (uint64_t)pe << 40 ^ i;
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    return (uint32_t)x;
+}
+
+struct Case {
+    int alg;
+    uint64_t n;
+    bool inplace;
+    unsigned soff, doff;  // byte offsets of src/dst in their heap regions
+};
+
+// One PE: `cases` calls in order, every result checked.
+void pe_main(int P, int me, const std::vector<Case> &cases, sosp2p::Shared *sh, long *ok_calls)
+{
+    Stream st;
+    CpuBackend be{&st};
+    sosp2p::Local loc;
+    char *heap = g_heaps[(size_t)me];
+    const size_t region = kHeap / 4;
+    std::vector<char> scratch_private;
+    uint64_t call = 0;
+    for (const Case &c : cases) {
+        ++call;
+        const uint64_t ts = 4, bytes = c.n * ts;
+        char *src = heap + c.soff;
+        char *dst = c.inplace ? src : heap + region + c.doff;
+        // this call's source (the caller's write, after the previous call returned)
+        for (uint64_t i = 0; i < c.n; ++i) {
+            const uint32_t v = val(call, me, i);
+            memcpy(src + 4 * i, &v, 4);
+        }
+        const uint32_t sentinel = 0xA5A5A5A5u;
+        if (!c.inplace)
+            for (uint64_t i = 0; i < c.n; ++i) memcpy(dst + 4 * i, &sentinel, 4);
+        const unsigned smis = (unsigned)((uintptr_t)src & 15), dmis = (unsigned)((uintptr_t)dst & 15);
+        sosplan::Plan plan;
+        if (sosplan::build(c.alg, P, me, c.n, ts, smis, dmis, &plan) != SOSX_OK) die("plan", c.alg, P);
+        char *scr = nullptr;
+        uint64_t scr_off = 0;
+        if (plan.scratch_bytes) {
+            if (plan.scr_sent) {  // peers read it: in the heap, after both operands
+                scr_off = 2 * region;
+                if (scr_off + plan.scratch_bytes > kHeap) die("heap too small", (int)plan.scratch_bytes);
+                scr = heap + scr_off;
+            } else {
+                scratch_private.assign(plan.scratch_bytes + 64, 0);
+                scr = scratch_private.data();
+            }
+        }
+        const sosp2p::Bufs b{src, dst, scr, (uint64_t)(src - heap), (uint64_t)(dst - heap), scr_off, smis, dmis};
+        const int rc = sosp2p::exec_host(plan, P, me, [](int i) { return i; }, c.alg, c.n, ts, b, sh, loc, be);
+        if (rc) die("exec_host failed", rc);
+        // expected result at this PE
+        const bool bcast = c.alg >= 32;
+        const int root = bcast ? (c.alg - 32) >> 1 : 0;
+        const bool copy_root = bcast && ((c.alg - 32) & 1);
+        for (uint64_t i = 0; i < c.n; ++i) {
+            uint32_t want = 0, got;
+            if (c.alg == SOSX_PLAN_INSCAN || c.alg == SOSX_PLAN_EXSCAN) {
+                const int last = c.alg == SOSX_PLAN_INSCAN ? me : me - 1;
+                for (int p = 0; p <= last; ++p) want += val(call, p, i);
+            } else if (bcast) {
+                want = me != root ? val(call, root, i) : copy_root || c.inplace ? val(call, me, i) : sentinel;
+            } else {
+                for (int p = 0; p < P; ++p) want += val(call, p, i);
+            }
+            memcpy(&got, dst + 4 * i, 4);
+            if (got != want) die("wrong result", c.alg, (int)i);
+        }
+        ++*ok_calls;
+    }
+}
+
+}  // namespace
+
+int main(int argc, char **argv)
+{
+    const int iters = argc > 1 ? atoi(argv[1]) : 2;
+    long total = 0;
+    auto *sh = (sosp2p::Shared *)calloc(1, sizeof(sosp2p::Shared));
+    const int algs[] = {SOSX_ALG_RING, SOSX_ALG_RECDBL, SOSX_ALG_RECHALVING, SOSX_ALG_RECDBL_DIRECT,
+                        SOSX_ALG_RECDBL_GATHER, SOSX_PLAN_INSCAN, SOSX_PLAN_EXSCAN};
+    for (int P : {2, 3, 4, 5, 8, 12}) {
+        g_heaps.clear();
+        for (int q = 0; q < P; ++q) {
+            char *h = (char *)aligned_alloc(4096, kHeap);
+            memset(h, 0, kHeap);
+            g_heaps.push_back(h);
+        }
+        std::vector<Case> cases;
+        for (int it = 0; it < iters; ++it)
+            for (uint64_t n : {1ull, 7ull, 1001ull, 65539ull}) {
+                for (int alg : algs)
+                    for (int inplace = 0; inplace < 2; ++inplace)
+                        cases.push_back(Case{alg, n, inplace != 0, inplace ? 4u * (unsigned)it % 16 : 0u,
+                                             inplace ? 0u : 8u});
+                for (int root : {0, P - 1})
+                    for (int copy = 0; copy < 2; ++copy)
+                        cases.push_back(Case{SOSX_PLAN_BCAST(root, copy), n, false, 0, 4});
+            }
+        // every PE starts with fresh counters: a new job
+        memset((void *)sh, 0, sizeof(*sh));
+        std::vector<long> ok((size_t)P, 0);
+        std::vector<std::thread> th;
+        for (int q = 0; q < P; ++q) th.emplace_back(pe_main, P, q, std::cref(cases), sh, &ok[(size_t)q]);
+        for (auto &t : th) t.join();
+        for (long v : ok) total += v;
+        for (char *h : g_heaps) free(h);
+    }
+    free(sh);
+    printf("p2p protocol harness: %ld calls OK\n", total);
+    return 0;
+}
