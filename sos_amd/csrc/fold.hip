@@ -116,9 +116,9 @@ int launch_fold_dyn(T *out, const FoldPtrs &ins, int np, size_t n, hipStream_t s
     return hip_ok(hipGetLastError());
 }
 
-// Some inputs at another 16-B offset than the output (all element-aligned), LINEAR order:
-// 16-B vectors, the incongruent inputs realigned in registers (fold_kernels.h).
-template <class T, class OP>
+// Some inputs at another 16-B offset than the output (all element-aligned), either
+// order: 16-B vectors, the incongruent inputs realigned in registers (fold_kernels.h).
+template <class T, class OP, int ORDER>
 int launch_fold_realign(T *out, const FoldPtrs &ins, int np, size_t n, hipStream_t st)
 {
     Geom g = make_geom((uintptr_t)out, n, sizeof(T), 1);
@@ -129,7 +129,7 @@ int launch_fold_realign(T *out, const FoldPtrs &ins, int np, size_t n, hipStream
         a.p[k] = ins.p[k];
         a.d[k] = (unsigned)((uintptr_t)((const T *)ins.p[k] + g.head) & 15);
     }
-    hipLaunchKernelGGL((k_fold_realign<T, OP>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st,
+    hipLaunchKernelGGL((k_fold_realign<T, OP, ORDER>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st,
                        out, a, g);
     return hip_ok(hipGetLastError());
 }
@@ -144,12 +144,11 @@ int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
         congruent &= (((uintptr_t)ins.p[k] ^ o) & 15) == 0;
         elem_aligned &= ((uintptr_t)ins.p[k] % sizeof(T)) == 0;
     }
-    // the LINEAR order only: that is the ring's fold, SOS AUTO's schedule for every size
-    // past the crossover (src/shmem_collectives.h:192-199); the TREE folds of large
-    // vectors (schedules forced by SHMEM_REDUCE_ALGORITHM) keep the element loop
-    if constexpr (ORDER == SOSX_ORDER_LINEAR)
-        if (!congruent && elem_aligned && n * sizeof(T) > kSpreadBytes)
-            return launch_fold_realign<T, OP>(out, ins, NP, n, st);
+    // both orders: the LINEAR one is the ring's fold (SOS AUTO past the crossover,
+    // src/shmem_collectives.h:192-199), the TREE one recdbl_sw's (AUTO below a raised
+    // SHMEM_COLL_SIZE_CROSSOVER, or SHMEM_REDUCE_ALGORITHM=recdbl/linear/tree)
+    if (!congruent && elem_aligned && n * sizeof(T) > kSpreadBytes)
+        return launch_fold_realign<T, OP, ORDER>(out, ins, NP, n, st);
     if (!congruent || n * sizeof(T) <= kSpreadBytes) return launch_fold_dyn<T, OP, ORDER>(out, ins, NP, n, st);
     constexpr int U = NP <= 2 ? 4 : (NP <= 4 ? 2 : 1);
     Geom g = make_geom(o, n, sizeof(T), U);

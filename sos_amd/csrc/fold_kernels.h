@@ -94,14 +94,16 @@ __global__ __launch_bounds__(kThreads) void k_fold(T *out, FoldPtrs ins, Geom g)
 }
 
 // ---------------------------------------------------------------------------------
-// The ring's LINEAR fold (2 <= P <= 8, at run time) when some inputs are NOT 16-B
-// congruent with the output: a team reduction whose source and target sit at different
-// 16-B offsets (the PE's own source chunk, or the peers' sources read in place, against
-// exchange scratch congruent with the target).  16-B vectors throughout: an input at
-// byte offset d[k] != 0 is read as the two aligned vectors its bytes straddle and
-// funnel-shifted into place (realign16; see k_combine3_realign for why the extra bytes
-// are safe to load).  acc = in[0] OP in[1] OP ... as fold_elem's LINEAR order, with P at
-// run time on compile-time indices, so one kernel per (type, op) serves every P.
+// The P-way fold (2 <= P <= 8, at run time) when some inputs are NOT 16-B congruent with
+// the output: a team reduction whose source and target sit at different 16-B offsets
+// (the PE's own source chunk, or the peers' sources read in place, against exchange
+// scratch congruent with the target).  16-B vectors throughout: an input at byte offset
+// d[k] != 0 is read as the two aligned vectors its bytes straddle and funnel-shifted
+// into place (realign16; see k_combine3_realign for why the extra bytes are safe to
+// load).  LINEAR: acc = in[0] OP in[1] OP ... (the ring); TREE: the recdbl_sw tree of
+// fold_elem (the extras folded into the first P - p2 leaves, then distance 1, 2, 4 pairs,
+// the lower subtree the left operand) -- with P at run time on compile-time indices, so
+// one kernel per (type, op, order) serves every P.
 // ---------------------------------------------------------------------------------
 struct FoldRealignArgs {
     const void *p[8];
@@ -109,7 +111,54 @@ struct FoldRealignArgs {
     int np;
 };
 
-template <class T, class OP>
+template <class T, class OP, int ORDER>
+__device__ __forceinline__ u32x4 fold_runtime_np(u32x4 (&x)[8], int np)
+{
+    if constexpr (ORDER == SOSX_ORDER_LINEAR) {
+        u32x4 acc = x[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k)
+            if (k < np) acc = apply<T, OP>(acc, x[k]);
+        return acc;
+    } else {
+        const int p2 = np >= 8 ? 8 : np >= 4 ? 4 : 2;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < np - p2) x[k] = apply<T, OP>(x[k], x[k + p2]);
+#pragma unroll
+        for (int d = 1; d < 8; d <<= 1)
+#pragma unroll
+            for (int k = 0; k < 8; k += 2 * d)
+                if (d < p2 && k < p2) x[k] = apply<T, OP>(x[k], x[k + d]);
+        return x[0];
+    }
+}
+
+template <class T, class OP, int ORDER>
+__device__ __forceinline__ T fold_runtime_np_elem(const FoldRealignArgs &a, size_t i)
+{
+    T v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = k < a.np ? ((const T *)a.p[k])[i] : T();
+    if constexpr (ORDER == SOSX_ORDER_LINEAR) {
+        T acc = v[0];
+        for (int k = 1; k < a.np; ++k) acc = OP::f(acc, v[k]);
+        return acc;
+    } else {
+        const int p2 = a.np >= 8 ? 8 : a.np >= 4 ? 4 : 2;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < a.np - p2) v[k] = OP::f(v[k], v[k + p2]);
+#pragma unroll
+        for (int d = 1; d < 8; d <<= 1)
+#pragma unroll
+            for (int k = 0; k < 8; k += 2 * d)
+                if (d < p2 && k < p2) v[k] = OP::f(v[k], v[k + d]);
+        return v[0];
+    }
+}
+
+template <class T, class OP, int ORDER = SOSX_ORDER_LINEAR>
 __global__ __launch_bounds__(kThreads) void k_fold_realign(T *out, FoldRealignArgs a, Geom g)
 {
     constexpr int V = Pack<T>::N;
@@ -129,21 +178,12 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign(T *out, FoldRealignAr
                 x[k] = d ? realign16(lo, ldv<true>(I + i + 1), d) : lo;
             }
         }
-        u32x4 acc = x[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k)
-            if (k < np) acc = apply<T, OP>(acc, x[k]);
-        stv<true>(O + i, acc);
+        stv<true>(O + i, fold_runtime_np<T, OP, ORDER>(x, np));
     }
     if (g.has_rem && blockIdx.x == nblk - 1) {
-        auto one = [&](size_t i) {
-            T acc = ((const T *)a.p[0])[i];
-            for (int k = 1; k < np; ++k) acc = OP::f(acc, ((const T *)a.p[k])[i]);
-            out[i] = acc;
-        };
-        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = fold_runtime_np_elem<T, OP, ORDER>(a, i);
         for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
-            one(i);
+            out[i] = fold_runtime_np_elem<T, OP, ORDER>(a, i);
     }
 }
 

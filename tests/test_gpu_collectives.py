@@ -127,20 +127,22 @@ def test_fold_runtime_p(torch_cuda, P, order, dt, op):
     assert np.array_equal(bits(from_dev(out, ref)), bits(ref))
 
 
-@pytest.mark.parametrize("P", [2, 3, 5, 8])
+@pytest.mark.parametrize("P", [2, 3, 5, 6, 7, 8])
 @pytest.mark.parametrize("dt,op", [(23, 5), (18, 5), (3, 2), (24, 6), (11, 4), (26, 5)])
 @pytest.mark.parametrize("layout", ["own", "peers", "mixed"])
-def test_fold_realigned_inputs(torch_cuda, P, dt, op, layout):
-    """LINEAR folds past 64 KiB per input whose inputs sit at other 16-B offsets than the
-    output (k_fold_realign): the PE's own source chunk only ("own", the ring at PE me with
-    source and target at different offsets), every input ("peers", the p2p transport's
-    in-place reads of the peers' sources), or each input at its own offset ("mixed");
-    ragged sizes; bit for bit against the plan simulator's LINEAR fold."""
+@pytest.mark.parametrize("order", [0, 1])
+def test_fold_realigned_inputs(torch_cuda, P, dt, op, layout, order):
+    """Folds past 64 KiB per input whose inputs sit at other 16-B offsets than the output
+    (k_fold_realign), in the ring's LINEAR order and in recdbl_sw's TREE order (the extras
+    first, then the pairwise tree): the PE's own source chunk only ("own", the ring at PE
+    me with source and target at different offsets), every input ("peers", the p2p
+    transport's in-place reads of the peers' sources), or each input at its own offset
+    ("mixed"); ragged sizes; bit for bit against the plan simulator's fold."""
     torch = torch_cuda
     es = O.lib().oracle_type_size(dt)
     for n in ((1 << 16) // es + 1, (1 << 20) + 3):
         ins = [O.fill(dt, 1 if op == 6 else 0, 11, k, n) for k in range(P)]
-        ref = plansim.fold_values(op, dt, ins, 0)
+        ref = plansim.fold_values(op, dt, ins, order)
         if layout == "own":
             offs = [es] + [0] * (P - 1)
         elif layout == "peers":
@@ -149,7 +151,7 @@ def test_fold_realigned_inputs(torch_cuda, P, dt, op, layout):
             offs = [(es * k) % 16 for k in range(1, P + 1)]
         di = [to_dev(torch, a, off) for a, off in zip(ins, offs)]
         out = torch.zeros_like(to_dev(torch, ins[0]))
-        _lib.fold(op, dt, 0, out.data_ptr(), [t.data_ptr() + off for t, off in zip(di, offs)], n)
+        _lib.fold(op, dt, order, out.data_ptr(), [t.data_ptr() + off for t, off in zip(di, offs)], n)
         torch.cuda.synchronize()
         assert np.array_equal(bits(from_dev(out, ref)), bits(ref)), (n, offs)
 
