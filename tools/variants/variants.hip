@@ -194,6 +194,83 @@ __global__ __launch_bounds__(kThreads) void k_fold_st(T *out, FoldPtrs ins, Geom
     }
 }
 
+// Lane-contiguous shapes: each lane reads U CONSECUTIVE 16-B vectors
+// of every input (lane l of tile t covers vectors (t * kThreads + l) * U .. + U - 1), so a
+// wave's U loads of one input cover U * 1 KiB contiguous with each lane's own 64 B run;
+// the default interleaves lanes (load u covers kThreads vectors at stride 1).  Same tile
+// geometry (make_geom with U), same element order.
+template <class T, class OP, int NP, int ORDER, int U>
+__global__ __launch_bounds__(kThreads) void k_fold_lc(T *out, FoldPtrs ins, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t base = (t * (size_t)kThreads + threadIdx.x) * U;
+        u32x4 x[U][NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const u32x4 *I = reinterpret_cast<const u32x4 *>((const T *)ins.p[k] + g.head);
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u][k] = ldv<true>(I + base + u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) stv<true>(O + base + u, fold_pack<T, OP, NP, ORDER>(x[u]));
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)ins.p[k])[i];
+            out[i] = fold_elem<T, OP, NP, ORDER>(v);
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
+template <class T, class OP, int NP, int U>
+__global__ __launch_bounds__(kThreads) void k_prefix_lc(PrefixPtrs p, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t base = (t * (size_t)kThreads + threadIdx.x) * U;
+        u32x4 x[U][NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                x[u][k] = ldv<true>(reinterpret_cast<const u32x4 *>((const T *)p.in[k] + g.head) + base + u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            u32x4 acc = x[u][0];
+            stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[0] + g.head) + base + u, acc);
+#pragma unroll
+            for (int k = 1; k < NP; ++k) {
+                acc = apply<T, OP>(acc, x[u][k]);
+                stv<true>(reinterpret_cast<u32x4 *>((T *)p.out[k] + g.head) + base + u, acc);
+            }
+        }
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)p.in[k])[i];
+            T acc = v[0];
+            ((T *)p.out[0])[i] = acc;
+#pragma unroll
+            for (int k = 1; k < NP; ++k) {
+                acc = OP::f(acc, v[k]);
+                ((T *)p.out[k])[i] = acc;
+            }
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * U * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
 }  // namespace sos
 
 using namespace sos;
@@ -283,12 +360,35 @@ int fold_st(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
     return hip_ok(hipGetLastError());
 }
 
-const char *const kFoldNames[] = {"u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd"};
-constexpr int kNumFold = 8;
+// Occupancy-capped shapes (round 5): the default kernel launched with `lds` bytes of
+// unused dynamic LDS, so at most 160 KiB / lds workgroups share a CU: fewer concurrent
+// workgroups, hence fewer DRAM rows open across the 9 (fold) or 16 (prefix) streams.
+template <int NP, int U>
+int fold_u_lds(T *out, const FoldPtrs &ins, size_t n, hipStream_t st, unsigned lds)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), U);
+    hipLaunchKernelGGL((k_fold<T, OP, NP, SOSX_ORDER_LINEAR, U>), dim3(grid_for(g, kNoCap)),
+                       dim3(kThreads), lds, st, out, ins, g);
+    return hip_ok(hipGetLastError());
+}
+
+template <int U>
+int fold_lc(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), U);
+    hipLaunchKernelGGL((k_fold_lc<T, OP, 8, SOSX_ORDER_LINEAR, U>), dim3(grid_for(g, kNoCap)),
+                       dim3(kThreads), 0, st, out, ins, g);
+    return hip_ok(hipGetLastError());
+}
+
+const char *const kFoldNames[] = {"u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd",
+                                  "lc2", "lc4", "u1_occ4", "u1_occ2", "u2_occ4"};
+constexpr int kNumFold = 13;
 
 const char *const kPrefixNames[] = {"u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain", "u8_nt",
-                                    "split2_nt", "split2_seed_plain"};
-constexpr int kNumPrefix = 8;
+                                    "split2_nt", "split2_seed_plain", "lc2", "lc4", "u1_occ4",
+                                    "u1_occ2"};
+constexpr int kNumPrefix = 12;
 
 // Continuation of a prefix from a seed vector: out[k] = seed OP in[0] OP ... OP in[k],
 // left to right, so the second half of a split prefix is bit-identical to the fused one
@@ -361,10 +461,31 @@ int prefix_u(const PrefixPtrs &p, size_t n, hipStream_t st)
     return hip_ok(hipGetLastError());
 }
 
+template <int NP, int U>
+int prefix_lc(const PrefixPtrs &p, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), U);
+    hipLaunchKernelGGL((k_prefix_lc<T, OP, NP, U>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st, p, g);
+    return hip_ok(hipGetLastError());
+}
+
+template <int NP>
+int prefix_lds(const PrefixPtrs &p, size_t n, hipStream_t st, unsigned lds)
+{
+    Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), 1);
+    hipLaunchKernelGGL((k_prefix<T, OP, NP, 1, true>), dim3(grid_for(g, kNoCap)), dim3(kThreads), lds,
+                       st, p, g);
+    return hip_ok(hipGetLastError());
+}
+
 template <int NP>
 int prefix_np(int v, const PrefixPtrs &p, size_t n, hipStream_t st)
 {
     switch (v) {
+        case 8: return prefix_lc<NP, 2>(p, n, st);
+        case 9: return prefix_lc<NP, 4>(p, n, st);
+        case 10: return prefix_lds<NP>(p, n, st, 40 << 10);
+        case 11: return prefix_lds<NP>(p, n, st, 64 << 10);
         case 0: return prefix_u<NP, 1, true>(p, n, st);
         case 1: return prefix_u<NP, 2, true>(p, n, st);
         case 2: return prefix_u<NP, 4, true>(p, n, st);
@@ -457,6 +578,11 @@ int sosxv_fold(int v, float *out, const void *const *ins, size_t n, void *stream
         case 5: return fold_st<1, false, true>(out, fp, n, st);
         case 6: return fold_st<4, true, false>(out, fp, n, st);
         case 7: return fold_st<16, true, true>(out, fp, n, st);
+        case 8: return fold_lc<2>(out, fp, n, st);
+        case 9: return fold_lc<4>(out, fp, n, st);
+        case 10: return fold_u_lds<8, 1>(out, fp, n, st, 40 << 10);
+        case 11: return fold_u_lds<8, 1>(out, fp, n, st, 64 << 10);
+        case 12: return fold_u_lds<8, 2>(out, fp, n, st, 40 << 10);
     }
     return SOSX_ERR_ARG;
 }
