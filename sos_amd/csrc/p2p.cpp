@@ -64,10 +64,7 @@ void prof_mark(int which, bool end, hipStream_t s);  // collectives.cpp (0 = fol
 namespace {
 
 using sosp2p::kMaxPE;
-using sosp2p::kDescRing;
-using sosp2p::Desc;
 using P2PShared = sosp2p::Shared;
-using sosp2p::round_fusable;
 
 sosp2p::Local g_local;
 
@@ -78,9 +75,7 @@ struct Sig {
     bool registered = false;
     char *dbase = nullptr;          // device view of the shared segment
     long long limit_ticks = 0;      // device wall-clock ticks of SHMEMX_P2P_TIMEOUT
-    uint64_t posted[kMaxPE] = {0};  // my sends to each world PE (cumulative)
-    uint64_t seen[kMaxPE] = {0};    // sends from each world PE I have waited for
-    uint64_t desc_sent[kMaxPE] = {0}, desc_got[kMaxPE] = {0};
+    sosp2p::StreamLocal sl;         // pair counters and descriptor indices (cumulative)
 };
 Sig g_sig;
 
@@ -207,16 +202,6 @@ bool trace_on()
     return g_trace.every > 0;
 }
 
-// The sends peer q's plan makes to `me`, in order (p2p_proto.h), or the end of the job.
-const std::vector<sosp2p::PeerSend> &peer_sends(int alg, int P, int q, int me, uint64_t count,
-                                                uint64_t ts, uint64_t mis)
-{
-    bool ok;
-    const auto &v = sosp2p::peer_sends(alg, P, q, me, count, ts, mis, &ok);
-    if (!ok) raise_error("p2p transport: cannot build the plan of PE %d", q);
-    return v;
-}
-
 }  // namespace
 
 size_t p2p_shared_bytes() { return sizeof(P2PShared); }
@@ -269,237 +254,6 @@ int run_round_ops(const sosplan::Round &r, const std::vector<std::vector<const v
         if (rc) return rc;
     }
     return SOSX_OK;
-}
-
-// Stream-mode executor: the whole call is enqueued at once (see the header).
-int p2p_exec_stream(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count,
-                    uint64_t ts, const P2PBufs &b, int op, int dt, hipStream_t stream)
-{
-    State &s = st();
-    P2PShared *sh = shared();
-    const int me = t.my_idx;
-    const int my_world = t.world_rank(me);
-    const bool tr = trace_on();
-    double tp = tr ? now_s() : 0;
-    auto phase = [&](int ph) {
-        if (!tr) return;
-        const double now = now_s();
-        g_trace.t[ph] += now - tp;
-        tp = now;
-    };
-    std::function<char *(int, uint64_t)> local_ptr = [&](int buf, uint64_t off) -> char * {
-        return (buf == sosplan::SRC ? (char *)b.src : buf == sosplan::DST ? b.dst : b.scr) + off;
-    };
-    // 1. descriptors: publish this call's offsets to every PE this call sends to, then
-    //    read those of every PE it receives from (host handshake, no GPU wait)
-    std::vector<char> sends_to((size_t)t.size, 0), recvs_from((size_t)t.size, 0);
-    for (const auto &r : plan.rounds)
-        for (const auto &x : r.xfers) (x.send ? sends_to : recvs_from)[(size_t)x.peer] = 1;
-    const Desc mine{b.src_off, b.dst_off, b.scr_off,
-                    (uint64_t)(b.smis & 15) | (uint64_t)(b.dmis & 15) << 4};
-    for (int q = 0; q < t.size; ++q) {
-        if (!sends_to[(size_t)q]) continue;
-        const int pw = t.world_rank(q);
-        const uint64_t idx = g_sig.desc_sent[pw]++;
-        if (idx >= (uint64_t)kDescRing)
-            spin_until(sh->desc_read[my_world][pw], idx + 1 - kDescRing, "a peer to take a descriptor");
-        sh->desc[my_world][pw][idx % kDescRing] = mine;
-        sh->desc_posted[my_world][pw].store(idx + 1, std::memory_order_release);
-    }
-    std::vector<Desc> peer_desc((size_t)t.size);
-    for (int q = 0; q < t.size; ++q) {
-        if (!recvs_from[(size_t)q]) continue;
-        const int pw = t.world_rank(q);
-        const uint64_t idx = g_sig.desc_got[pw]++;
-        spin_until(sh->desc_posted[pw][my_world], idx + 1, "a peer's call descriptor");
-        peer_desc[(size_t)q] = sh->desc[pw][my_world][idx % kDescRing];
-        sh->desc_read[pw][my_world].store(idx + 1, std::memory_order_release);
-    }
-    phase(PH_WAIT_POST);
-    // pending signalling step: stores first, then waits (merged across a round boundary
-    // when no local op sits between them)
-    std::map<uint64_t *, uint64_t> pw_store;
-    std::map<const uint64_t *, uint64_t> pw_wait;
-    auto flush = [&]() -> int {
-        if (pw_store.empty() && pw_wait.empty()) return SOSX_OK;
-        // posts make the bytes of this round's sends readable by peers, on other GPUs
-        // over xGMI: a system-scope release in stream order first (release_system)
-        if (!pw_store.empty() && release_system(stream) != hipSuccess) return SOSX_ERR_HIP;
-        std::vector<uint64_t *> wa;
-        std::vector<uint64_t> wv;
-        std::vector<const uint64_t *> qa;
-        std::vector<uint64_t> qv;
-        for (auto &kv : pw_store) {
-            wa.push_back(dev(kv.first));
-            wv.push_back(kv.second);
-        }
-        for (auto &kv : pw_wait) {
-            qa.push_back(dev(kv.first));
-            qv.push_back(kv.second);
-        }
-        pw_store.clear();
-        pw_wait.clear();
-        return sosx_p2p_signal((int)wa.size(), wa.data(), wv.data(), (int)qa.size(), qa.data(),
-                               qv.data(), dev(&sh->sig_err[my_world]), g_sig.limit_ticks, stream);
-    };
-    // the same step done by the host (the call's first and last boundaries, where the
-    // host has nothing to overlap: stores, then bounded waits)
-    auto host_flush = [&]() {
-        for (auto &kv : pw_store) __atomic_store_n(kv.first, kv.second, __ATOMIC_RELEASE);
-        for (auto &kv : pw_wait) spin_until_u64(kv.first, kv.second, "a peer (call boundary)");
-        pw_store.clear();
-        pw_wait.clear();
-    };
-    std::vector<int> recv_idx((size_t)t.size, 0);  // k-th receive from each team peer
-    bool first_xfer_round = true;
-    for (const auto &r : plan.rounds) {
-        if (r.xfers.empty()) {
-            int rc = flush();
-            if (rc) return rc;
-            std::vector<std::vector<const void *>> ins(r.ops.size());
-            for (size_t i = 0; i < r.ops.size(); ++i)
-                for (int k = 0; k < r.ops[i].nin; ++k)
-                    ins[i].push_back(local_ptr(r.ops[i].in_buf[k], r.ops[i].in_off[k]));
-            rc = run_round_ops(r, ins, local_ptr, op, dt, stream);
-            if (rc) return rc;
-            continue;
-        }
-        // post this round's sends (their bytes are final in stream order), wait for the
-        // peers' posts of what this round receives
-        for (const auto &x : r.xfers) {
-            const int pw = t.world_rank(x.peer);
-            if (x.send) {
-                pw_store[&sh->dposted[my_world][pw]] = ++g_sig.posted[pw];
-            } else {
-                pw_wait[&sh->dposted[pw][my_world]] = ++g_sig.seen[pw];
-            }
-        }
-        int rc;
-        bool step_pending = false;  // the signalling step still to be enqueued
-        if (first_xfer_round) {
-            // the call's entry boundary runs on the host, as in host mode: nothing is
-            // queued ahead of it that a signal kernel could overlap (stream sync only
-            // when this round sends, so that the posted bytes are final)
-            first_xfer_round = false;
-            bool sends = false;
-            for (const auto &x : r.xfers) sends |= x.send != 0;
-            if (sends && sync_system(stream) != hipSuccess) return SOSX_ERR_HIP;
-            host_flush();
-            stall_hook();
-        } else {
-            step_pending = true;
-        }
-        struct Seg { const char *src; char *dst; uint64_t bytes; bool used; };
-        std::vector<Seg> segs;
-        for (const auto &x : r.xfers) {
-            if (x.send) continue;
-            const int pw = t.world_rank(x.peer);
-            const Desc &d = peer_desc[(size_t)x.peer];
-            const auto &sends = peer_sends(alg, t.size, x.peer, me, count, ts, d.mis);
-            const int k = recv_idx[(size_t)x.peer]++;
-            if (k >= (int)sends.size() || sends[(size_t)k].bytes != x.bytes)
-                raise_error("p2p transport: plan mismatch with PE %d", pw);
-            const sosp2p::PeerSend &ps = sends[(size_t)k];
-            const uint64_t boff = ps.buf == sosplan::SRC ? d.src_off
-                                : ps.buf == sosplan::DST ? d.dst_off : d.scr_off;
-            segs.push_back(Seg{s.peer_heap[(size_t)pw] + boff + ps.off, local_ptr(x.buf, x.off),
-                               x.bytes, false});
-        }
-        const bool fuse_ok = round_fusable(r, ts, local_ptr);
-        std::vector<std::vector<const void *>> ins(r.ops.size());
-        for (size_t i = 0; i < r.ops.size(); ++i) {
-            const auto &l = r.ops[i];
-            for (int k = 0; k < l.nin; ++k) {
-                const char *p = local_ptr(l.in_buf[k], l.in_off[k]);
-                if (fuse_ok && (l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX))
-                    for (auto &sg : segs)
-                        if (sg.dst == p && sg.bytes == l.count * ts) {
-                            p = sg.src;
-                            sg.used = true;
-                        }
-                ins[i].push_back(p);
-            }
-        }
-        std::vector<const void *> gs;
-        std::vector<void *> gd;
-        std::vector<size_t> gb;
-        for (auto &sg : segs)
-            if (!sg.used) {
-                gs.push_back(sg.src);
-                gd.push_back(sg.dst);
-                gb.push_back(sg.bytes);
-            }
-        if (step_pending && !gs.empty() && pw_store.size() <= 16 && pw_wait.size() <= 16) {
-            // the step rides in the gather launch (small grids; else its own launch)
-            std::vector<uint64_t *> wa;
-            std::vector<uint64_t> wv;
-            std::vector<const uint64_t *> qa;
-            std::vector<uint64_t> qv;
-            for (auto &kv : pw_store) {
-                wa.push_back(dev(kv.first));
-                wv.push_back(kv.second);
-            }
-            for (auto &kv : pw_wait) {
-                qa.push_back(dev(kv.first));
-                qv.push_back(kv.second);
-            }
-            pw_store.clear();
-            pw_wait.clear();
-            if (!wa.empty() && release_system(stream) != hipSuccess) return SOSX_ERR_HIP;
-            prof_mark(1, false, stream);
-            rc = sosx_gather_signalled((int)gs.size(), gs.data(), gd.data(), gb.data(),
-                                       (int)wa.size(), wa.data(), wv.data(), (int)qa.size(),
-                                       qa.data(), qv.data(), dev(&sh->sig_err[my_world]),
-                                       g_sig.limit_ticks, stream);
-            prof_mark(1, true, stream);
-            if (rc) return rc;
-        } else {
-            if (step_pending) {
-                rc = flush();
-                if (rc) return rc;
-            }
-            if (!gs.empty()) {
-                prof_mark(1, false, stream);
-                rc = sosx_gather((int)gs.size(), gs.data(), gd.data(), gb.data(), stream);
-                prof_mark(1, true, stream);
-                if (rc) return rc;
-            }
-        }
-        if (fuse_ok) {
-            rc = run_round_ops(r, ins, local_ptr, op, dt, stream);
-            if (rc) return rc;
-        }
-        // this round's receives are read: mark them consumed; this PE's sends must be
-        // consumed before anything overwrites them (the next round's ops or the caller)
-        for (const auto &x : r.xfers) {
-            const int pw = t.world_rank(x.peer);
-            if (x.send) pw_wait[&sh->dconsumed[my_world][pw]] = g_sig.posted[pw];
-            else pw_store[&sh->dconsumed[pw][my_world]] = g_sig.seen[pw];
-        }
-        if (!fuse_ok) {
-            rc = flush();
-            if (rc) return rc;
-            rc = run_round_ops(r, ins, local_ptr, op, dt, stream);
-            if (rc) return rc;
-        }
-    }
-    // the exit boundary (the last round's consumed marks) on the host, after the sync
-    phase(PH_ENQUEUE);
-    const hipError_t e = sync_system(stream);
-    if (__atomic_load_n(&sh->sig_err[my_world], __ATOMIC_ACQUIRE))
-        raise_error("p2p transport: timed out after %.0f s waiting for a peer (device wait)",
-                    wait_limit_s());
-    if (e == hipSuccess) host_flush();
-    phase(PH_SYNC_END);
-    if (tr && ++g_trace.calls % g_trace.every == 0) {
-        const double k = 1e6 / (double)g_trace.every;
-        fprintf(stderr, "[%04d] p2p trace, stream mode (calls %ld-%ld, us/call): descriptors %.1f "
-                "enqueue %.1f sync-end %.1f\n", s.my_pe, g_trace.calls - g_trace.every + 1,
-                g_trace.calls, g_trace.t[PH_WAIT_POST] * k, g_trace.t[PH_ENQUEUE] * k,
-                g_trace.t[PH_SYNC_END] * k);
-        for (double &v : g_trace.t) v = 0;
-    }
-    return e == hipSuccess ? SOSX_OK : SOSX_ERR_HIP;
 }
 
 }  // namespace
@@ -613,18 +367,36 @@ namespace sosrt {
 
 namespace {
 
-// The host-signalling protocol's backend on this PE's HIP stream (p2p_proto.h).
+// The protocol's backend on this PE's HIP stream (p2p_proto.h), both signalling modes.
 struct HipBackend {
     hipStream_t stream;
     int op, dt;
+    int my_world;
     double tp;
     bool tr;
     int complete() { return sosrt::complete(stream) == hipSuccess ? 0 : 1; }
     int drain() { return hipStreamSynchronize(stream) == hipSuccess ? 0 : 1; }
+    int release() { return release_system(stream) == hipSuccess ? 0 : 1; }
     int gather(int n, const void *const *srcs, void *const *dsts, const size_t *bytes)
     {
         prof_mark(1, false, stream);
         const int rc = sosx_gather(n, srcs, dsts, bytes, stream);
+        prof_mark(1, true, stream);
+        return rc;
+    }
+    int signal(int nw, uint64_t *const *wa, const uint64_t *wv, int nq, const uint64_t *const *qa,
+               const uint64_t *qv)
+    {
+        return sosx_p2p_signal(nw, wa, wv, nq, qa, qv, dev(&shared()->sig_err[my_world]),
+                               g_sig.limit_ticks, stream);
+    }
+    int gather_signalled(int n, const void *const *srcs, void *const *dsts, const size_t *bytes, int nw,
+                         uint64_t *const *wa, const uint64_t *wv, int nq, const uint64_t *const *qa,
+                         const uint64_t *qv)
+    {
+        prof_mark(1, false, stream);
+        const int rc = sosx_gather_signalled(n, srcs, dsts, bytes, nw, wa, wv, nq, qa, qv,
+                                             dev(&shared()->sig_err[my_world]), g_sig.limit_ticks, stream);
         prof_mark(1, true, stream);
         return rc;
     }
@@ -633,8 +405,19 @@ struct HipBackend {
     {
         return run_round_ops(r, ins, local_ptr, op, dt, stream);
     }
+    uint64_t *dev(uint64_t *p) { return sosrt::dev(p); }
+    const uint64_t *dev(const uint64_t *p) { return sosrt::dev(p); }
     const char *peer_base(int pw) { return st().peer_heap[(size_t)pw]; }
     void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what) { spin_until(a, want, what); }
+    void spin_u64(const uint64_t *a, uint64_t want, const char *what) { spin_until_u64(a, want, what); }
+    void entry_hook() { stall_hook(); }
+    bool device_wait_failed()
+    {
+        if (__atomic_load_n(&shared()->sig_err[my_world], __ATOMIC_ACQUIRE))
+            raise_error("p2p transport: timed out after %.0f s waiting for a peer (device wait)",
+                        wait_limit_s());
+        return false;
+    }
     void plan_mismatch(int pw) { raise_error("p2p transport: plan mismatch with PE %d", pw); }
     void phase(int ph)
     {
@@ -653,12 +436,23 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
     State &s = st();
     P2PShared *sh = shared();
     if (!sh) return SOSX_ERR_STATE;
-    if (g_sig.on) return p2p_exec_stream(plan, t, alg, count, ts, b, op, dt, stream);
     const bool tr = trace_on();
-    HipBackend be{stream, op, dt, tr ? now_s() : 0, tr};
+    HipBackend be{stream, op, dt, t.world_rank(t.my_idx), tr ? now_s() : 0, tr};
     const sosp2p::Bufs pb{b.src, b.dst, b.scr, b.src_off, b.dst_off, b.scr_off, b.smis, b.dmis};
-    const int rc = sosp2p::exec_host(plan, t.size, t.my_idx, [&](int i) { return t.world_rank(i); }, alg,
-                                     count, ts, pb, sh, g_local, be);
+    auto world_of = [&](int i) { return t.world_rank(i); };
+    if (g_sig.on) {
+        const int rc = sosp2p::exec_stream(plan, t.size, t.my_idx, world_of, alg, count, ts, pb, sh,
+                                           g_sig.sl, be);
+        if (tr && ++g_trace.calls % g_trace.every == 0) {
+            const double k = 1e6 / (double)g_trace.every;
+            fprintf(stderr, "[%04d] p2p trace, stream mode (calls %ld-%ld, us/call): descriptors %.1f "
+                    "enqueue %.1f sync-end %.1f\n", s.my_pe, g_trace.calls - g_trace.every + 1,
+                    g_trace.calls, g_trace.t[1] * k, g_trace.t[2] * k, g_trace.t[5] * k);
+            for (double &v : g_trace.t) v = 0;
+        }
+        return rc;
+    }
+    const int rc = sosp2p::exec_host(plan, t.size, t.my_idx, world_of, alg, count, ts, pb, sh, g_local, be);
     if (tr && ++g_trace.calls % g_trace.every == 0) {  // window averages, then reset
         const double k = 1e6 / (double)g_trace.every;
         fprintf(stderr, "[%04d] p2p trace (calls %ld-%ld, us/call): sync-send %.1f wait-post %.1f "

@@ -1,11 +1,12 @@
-// p2p_proto.h -- the peer-to-peer transport's pairing protocol in host-signalling mode,
-// written once over a backend: p2p.cpp instantiates it with the HIP stream (kernels,
+// p2p_proto.h -- the peer-to-peer transport's pairing protocol (host- and stream-signalling
+// modes), written once over a backend: p2p.cpp instantiates it with the HIP stream (kernels,
 // system-scope completion), tests/p2p_proto_harness.cpp with CPU threads and memcpy
 // (run under ThreadSanitizer: every byte a PE reads from a peer must be ordered after the
 // peer's writes by the protocol's release/acquire counters, and every overwrite after
 // the peers' reads).
 //
-// The protocol (see p2p.cpp's header): a transfer is a PULL.  Per round, at PE me:
+// The host-mode protocol (see p2p.cpp's header; stream mode: exec_stream below): a
+// transfer is a PULL.  Per round, at PE me:
 //   1. if the round sends: complete the stream (the sent bytes are final and in memory),
 //      then post every send (posted[me][to]++ , release);
 //   2. for every receive: wait for the peer's post (acquire), locate the bytes from the
@@ -62,6 +63,13 @@ struct Shared {
 struct Local {
     uint64_t posted_by_me[kMaxPE] = {0};      // posts I made to each peer
     uint64_t seen_from[kMaxPE] = {0};         // posts from each peer I have consumed
+};
+
+// The same for stream mode (cumulative device counters and descriptor ring indices).
+struct StreamLocal {
+    uint64_t posted[kMaxPE] = {0};  // my sends to each world PE (cumulative)
+    uint64_t seen[kMaxPE] = {0};    // sends from each world PE I have waited for
+    uint64_t desc_sent[kMaxPE] = {0}, desc_got[kMaxPE] = {0};
 };
 
 // One call's buffers at this PE: addresses, and the heap offsets the peers rebuild them from.
@@ -240,6 +248,213 @@ int exec_host(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of,
         }
     }
     const int e = be.complete();  // the caller's result in memory
+    be.phase(PH_SYNC_END);
+    return e == 0 ? SOSX_OK : SOSX_ERR_HIP;
+}
+
+// Stream-signalled executor (stream mode, p2p.cpp's header): the whole call is enqueued
+// at once.  The call's offsets travel ahead through a descriptor ring per ordered pair
+// (host handshake, never waiting on a GPU); between rounds the pair counters move in
+// stream order (a signal step: stores, then bounded waits), carried by a small gather's
+// own launch when it can; the call's entry and exit boundaries run on the host.
+// Backend B adds to exec_host's:
+//   int release()                     a system-scope release in stream order
+//   int signal(nw, waddr, wval, nq, qaddr, qval)              one queued step
+//   int gather_signalled(n, srcs, dsts, bytes, nw, waddr, wval, nq, qaddr, qval)
+//   uint64_t *dev(uint64_t *), const uint64_t *dev(const uint64_t *)   the step's view
+//   void spin_u64(const uint64_t *a, uint64_t want, const char *what)  host wait
+//   void entry_hook()                 after the entry boundary (test hook)
+//   bool device_wait_failed()         a queued wait timed out (after complete())
+template <class B, class WorldOf>
+int exec_stream(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of, int alg,
+                uint64_t count, uint64_t ts, const Bufs &b, Shared *sh, StreamLocal &sl, B &be)
+{
+    enum { PH_WAIT_POST = 1, PH_ENQUEUE = 2, PH_SYNC_END = 5 };
+    const int my_world = world_of(me);
+    LocalPtr local_ptr = [&](int buf, uint64_t off) -> char * {
+        return (buf == sosplan::SRC ? (char *)b.src : buf == sosplan::DST ? b.dst : b.scr) + off;
+    };
+    // 1. descriptors: publish this call's offsets to every PE this call sends to, then
+    //    read those of every PE it receives from
+    std::vector<char> sends_to((size_t)P, 0), recvs_from((size_t)P, 0);
+    for (const auto &r : plan.rounds)
+        for (const auto &x : r.xfers) (x.send ? sends_to : recvs_from)[(size_t)x.peer] = 1;
+    const Desc mine{b.src_off, b.dst_off, b.scr_off,
+                    (uint64_t)(b.smis & 15) | (uint64_t)(b.dmis & 15) << 4};
+    for (int q = 0; q < P; ++q) {
+        if (!sends_to[(size_t)q]) continue;
+        const int pw = world_of(q);
+        const uint64_t idx = sl.desc_sent[pw]++;
+        if (idx >= (uint64_t)kDescRing)
+            be.spin(sh->desc_read[my_world][pw], idx + 1 - kDescRing, "a peer to take a descriptor");
+        sh->desc[my_world][pw][idx % kDescRing] = mine;
+        sh->desc_posted[my_world][pw].store(idx + 1, std::memory_order_release);
+    }
+    std::vector<Desc> peer_desc((size_t)P);
+    for (int q = 0; q < P; ++q) {
+        if (!recvs_from[(size_t)q]) continue;
+        const int pw = world_of(q);
+        const uint64_t idx = sl.desc_got[pw]++;
+        be.spin(sh->desc_posted[pw][my_world], idx + 1, "a peer's call descriptor");
+        peer_desc[(size_t)q] = sh->desc[pw][my_world][idx % kDescRing];
+        sh->desc_read[pw][my_world].store(idx + 1, std::memory_order_release);
+    }
+    be.phase(PH_WAIT_POST);
+    // pending signalling step: stores first, then waits (merged across a round boundary
+    // when no local op sits between them)
+    std::map<uint64_t *, uint64_t> pw_store;
+    std::map<const uint64_t *, uint64_t> pw_wait;
+    auto take = [&](std::vector<uint64_t *> &wa, std::vector<uint64_t> &wv,
+                    std::vector<const uint64_t *> &qa, std::vector<uint64_t> &qv) {
+        for (auto &kv : pw_store) {
+            wa.push_back(be.dev(kv.first));
+            wv.push_back(kv.second);
+        }
+        for (auto &kv : pw_wait) {
+            qa.push_back(be.dev(kv.first));
+            qv.push_back(kv.second);
+        }
+        pw_store.clear();
+        pw_wait.clear();
+    };
+    auto flush = [&]() -> int {
+        if (pw_store.empty() && pw_wait.empty()) return SOSX_OK;
+        // posts make the bytes of this round's sends readable by peers, on other GPUs
+        // over xGMI: a system-scope release in stream order first
+        if (!pw_store.empty() && be.release() != 0) return SOSX_ERR_HIP;
+        std::vector<uint64_t *> wa;
+        std::vector<uint64_t> wv;
+        std::vector<const uint64_t *> qa;
+        std::vector<uint64_t> qv;
+        take(wa, wv, qa, qv);
+        return be.signal((int)wa.size(), wa.data(), wv.data(), (int)qa.size(), qa.data(), qv.data());
+    };
+    // the same step done by the host (the call's first and last boundaries)
+    auto host_flush = [&]() {
+        for (auto &kv : pw_store) __atomic_store_n(kv.first, kv.second, __ATOMIC_RELEASE);
+        for (auto &kv : pw_wait) be.spin_u64(kv.first, kv.second, "a peer (call boundary)");
+        pw_store.clear();
+        pw_wait.clear();
+    };
+    std::vector<int> recv_idx((size_t)P, 0);  // k-th receive from each team peer
+    bool first_xfer_round = true;
+    for (const auto &r : plan.rounds) {
+        if (r.xfers.empty()) {
+            int rc = flush();
+            if (rc) return rc;
+            std::vector<std::vector<const void *>> ins(r.ops.size());
+            for (size_t i = 0; i < r.ops.size(); ++i)
+                for (int k = 0; k < r.ops[i].nin; ++k)
+                    ins[i].push_back(local_ptr(r.ops[i].in_buf[k], r.ops[i].in_off[k]));
+            rc = be.run_ops(r, ins, local_ptr);
+            if (rc) return rc;
+            continue;
+        }
+        // post this round's sends (their bytes are final in stream order), wait for the
+        // peers' posts of what this round receives
+        for (const auto &x : r.xfers) {
+            const int pw = world_of(x.peer);
+            if (x.send) pw_store[&sh->dposted[my_world][pw]] = ++sl.posted[pw];
+            else pw_wait[&sh->dposted[pw][my_world]] = ++sl.seen[pw];
+        }
+        int rc;
+        bool step_pending = false;  // the signalling step still to be enqueued
+        if (first_xfer_round) {
+            // the entry boundary runs on the host: nothing is queued ahead of it that a
+            // signal step could overlap (complete only when this round sends)
+            first_xfer_round = false;
+            bool sends = false;
+            for (const auto &x : r.xfers) sends |= x.send != 0;
+            if (sends && be.complete() != 0) return SOSX_ERR_HIP;
+            host_flush();
+            be.entry_hook();
+        } else {
+            step_pending = true;
+        }
+        struct Seg { const char *src; char *dst; uint64_t bytes; bool used; };
+        std::vector<Seg> segs;
+        for (const auto &x : r.xfers) {
+            if (x.send) continue;
+            const int pw = world_of(x.peer);
+            const Desc &d = peer_desc[(size_t)x.peer];
+            bool ok;
+            const auto &sends = peer_sends(alg, P, x.peer, me, count, ts, d.mis, &ok);
+            const int k = recv_idx[(size_t)x.peer]++;
+            if (!ok || k >= (int)sends.size() || sends[(size_t)k].bytes != x.bytes) be.plan_mismatch(pw);
+            const PeerSend &ps = sends[(size_t)k];
+            const uint64_t boff = ps.buf == sosplan::SRC ? d.src_off
+                                : ps.buf == sosplan::DST ? d.dst_off : d.scr_off;
+            segs.push_back(Seg{be.peer_base(pw) + boff + ps.off, local_ptr(x.buf, x.off), x.bytes, false});
+        }
+        const bool fuse_ok = round_fusable(r, ts, local_ptr);
+        std::vector<std::vector<const void *>> ins(r.ops.size());
+        for (size_t i = 0; i < r.ops.size(); ++i) {
+            const auto &l = r.ops[i];
+            for (int k = 0; k < l.nin; ++k) {
+                const char *p = local_ptr(l.in_buf[k], l.in_off[k]);
+                if (fuse_ok && (l.kind == sosplan::FOLD || l.kind == sosplan::PREFIX))
+                    for (auto &sg : segs)
+                        if (sg.dst == p && sg.bytes == l.count * ts) {
+                            p = sg.src;
+                            sg.used = true;
+                        }
+                ins[i].push_back(p);
+            }
+        }
+        std::vector<const void *> gs;
+        std::vector<void *> gd;
+        std::vector<size_t> gb;
+        for (auto &sg : segs)
+            if (!sg.used) {
+                gs.push_back(sg.src);
+                gd.push_back(sg.dst);
+                gb.push_back(sg.bytes);
+            }
+        if (step_pending && !gs.empty() && pw_store.size() <= 16 && pw_wait.size() <= 16) {
+            // the step rides in the gather launch (small grids; else its own launch)
+            const bool posts = !pw_store.empty();
+            std::vector<uint64_t *> wa;
+            std::vector<uint64_t> wv;
+            std::vector<const uint64_t *> qa;
+            std::vector<uint64_t> qv;
+            take(wa, wv, qa, qv);
+            if (posts && be.release() != 0) return SOSX_ERR_HIP;
+            rc = be.gather_signalled((int)gs.size(), gs.data(), gd.data(), gb.data(), (int)wa.size(),
+                                     wa.data(), wv.data(), (int)qa.size(), qa.data(), qv.data());
+            if (rc) return rc;
+        } else {
+            if (step_pending) {
+                rc = flush();
+                if (rc) return rc;
+            }
+            if (!gs.empty()) {
+                rc = be.gather((int)gs.size(), gs.data(), gd.data(), gb.data());
+                if (rc) return rc;
+            }
+        }
+        if (fuse_ok) {
+            rc = be.run_ops(r, ins, local_ptr);
+            if (rc) return rc;
+        }
+        // this round's receives are read: mark them consumed; this PE's sends must be
+        // consumed before anything overwrites them (the next round's ops or the caller)
+        for (const auto &x : r.xfers) {
+            const int pw = world_of(x.peer);
+            if (x.send) pw_wait[&sh->dconsumed[my_world][pw]] = sl.posted[pw];
+            else pw_store[&sh->dconsumed[pw][my_world]] = sl.seen[pw];
+        }
+        if (!fuse_ok) {
+            rc = flush();
+            if (rc) return rc;
+            rc = be.run_ops(r, ins, local_ptr);
+            if (rc) return rc;
+        }
+    }
+    // the exit boundary (the last round's consumed marks) on the host, after completion
+    be.phase(PH_ENQUEUE);
+    const int e = be.complete();
+    if (be.device_wait_failed()) return SOSX_ERR_STATE;
+    if (e == 0) host_flush();
     be.phase(PH_SYNC_END);
     return e == 0 ? SOSX_OK : SOSX_ERR_HIP;
 }

@@ -1,5 +1,6 @@
-// p2p_proto_harness.cpp -- the p2p transport's host-signalling protocol (the product's own
-// sosp2p::exec_host, sos_amd/csrc/p2p_proto.h) on CPU threads, for ThreadSanitizer.
+// p2p_proto_harness.cpp -- the p2p transport's pairing protocol in both signalling modes
+// (the product's own sosp2p::exec_host and sosp2p::exec_stream, sos_amd/csrc/p2p_proto.h)
+// on CPU threads, for ThreadSanitizer.
 //
 // Test infrastructure (tests/test_p2p_proto.py builds and runs it; no GPU).  Each PE is a
 // host thread with a "stream": a worker thread that runs the PE's queued copies and folds
@@ -9,7 +10,9 @@
 // independent, so every schedule's result is the plain sum / prefix / root's bytes).
 // Every call's result is checked; under -fsanitize=thread every byte a worker reads from
 // a peer must be ordered after the peer's writes, and every overwrite after the peers'
-// reads, by the protocol's counters alone.
+// reads, by the protocol's counters alone.  In stream mode the signal steps are queued on
+// the worker like any kernel: their stores and (blocking) waits run in stream order, as
+// the GPU's k_p2p_signal does, so a step that waits too early deadlocks here as there.
 //
 // Build with -DBROKEN_DRAIN to drop the drain before a round's receives are marked
 // consumed (step 4): the sanitizer must then report the race (the negative control).
@@ -158,6 +161,48 @@ struct CpuBackend {
         }
         return 0;
     }
+    // stream mode
+    int release() { return 0; }  // stream order is program order on the worker
+    static void step(const std::vector<uint64_t *> &wa, const std::vector<uint64_t> &wv,
+                     const std::vector<const uint64_t *> &qa, const std::vector<uint64_t> &qv)
+    {
+        for (size_t i = 0; i < wa.size(); ++i) __atomic_store_n(wa[i], wv[i], __ATOMIC_RELEASE);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (size_t i = 0; i < qa.size(); ++i)
+            while (__atomic_load_n(qa[i], __ATOMIC_ACQUIRE) < qv[i]) {
+                std::this_thread::yield();
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) die("device wait");
+            }
+    }
+    int signal(int nw, uint64_t *const *wa, const uint64_t *wv, int nq, const uint64_t *const *qa,
+               const uint64_t *qv)
+    {
+        std::vector<uint64_t *> a(wa, wa + nw);
+        std::vector<uint64_t> av(wv, wv + nw);
+        std::vector<const uint64_t *> q(qa, qa + nq);
+        std::vector<uint64_t> qv2(qv, qv + nq);
+        s->push([a, av, q, qv2] { step(a, av, q, qv2); });
+        return 0;
+    }
+    int gather_signalled(int n, const void *const *srcs, void *const *dsts, const size_t *bytes, int nw,
+                         uint64_t *const *wa, const uint64_t *wv, int nq, const uint64_t *const *qa,
+                         const uint64_t *qv)
+    {
+        signal(nw, wa, wv, nq, qa, qv);
+        return gather(n, srcs, dsts, bytes);
+    }
+    uint64_t *dev(uint64_t *p) { return p; }
+    const uint64_t *dev(const uint64_t *p) { return p; }
+    void spin_u64(const uint64_t *a, uint64_t want, const char *what)
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(a, __ATOMIC_ACQUIRE) < want) {
+            std::this_thread::yield();
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) die(what);
+        }
+    }
+    void entry_hook() {}
+    bool device_wait_failed() { return false; }
     const char *peer_base(int pw) { return g_heaps[(size_t)pw]; }
     void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what)
     {
@@ -188,11 +233,13 @@ struct Case {
 };
 
 // One PE: `cases` calls in order, every result checked.
-void pe_main(int P, int me, const std::vector<Case> &cases, sosp2p::Shared *sh, long *ok_calls)
+void pe_main(int P, int me, bool stream_mode, const std::vector<Case> &cases, sosp2p::Shared *sh,
+             long *ok_calls)
 {
     Stream st;
     CpuBackend be{&st};
     sosp2p::Local loc;
+    sosp2p::StreamLocal sl;
     char *heap = g_heaps[(size_t)me];
     const size_t region = kHeap / 4;
     std::vector<char> scratch_private;
@@ -226,7 +273,10 @@ void pe_main(int P, int me, const std::vector<Case> &cases, sosp2p::Shared *sh, 
             }
         }
         const sosp2p::Bufs b{src, dst, scr, (uint64_t)(src - heap), (uint64_t)(dst - heap), scr_off, smis, dmis};
-        const int rc = sosp2p::exec_host(plan, P, me, [](int i) { return i; }, c.alg, c.n, ts, b, sh, loc, be);
+        auto world_of = [](int i) { return i; };
+        const int rc = stream_mode
+                           ? sosp2p::exec_stream(plan, P, me, world_of, c.alg, c.n, ts, b, sh, sl, be)
+                           : sosp2p::exec_host(plan, P, me, world_of, c.alg, c.n, ts, b, sh, loc, be);
         if (rc) die("exec_host failed", rc);
         // expected result at this PE
         const bool bcast = c.alg >= 32;
@@ -258,6 +308,7 @@ int main(int argc, char **argv)
     auto *sh = (sosp2p::Shared *)calloc(1, sizeof(sosp2p::Shared));
     const int algs[] = {SOSX_ALG_RING, SOSX_ALG_RECDBL, SOSX_ALG_RECHALVING, SOSX_ALG_RECDBL_DIRECT,
                         SOSX_ALG_RECDBL_GATHER, SOSX_PLAN_INSCAN, SOSX_PLAN_EXSCAN};
+    for (int mode = 0; mode < 2; ++mode)
     for (int P : {2, 3, 4, 5, 8, 12}) {
         g_heaps.clear();
         for (int q = 0; q < P; ++q) {
@@ -280,12 +331,13 @@ int main(int argc, char **argv)
         memset((void *)sh, 0, sizeof(*sh));
         std::vector<long> ok((size_t)P, 0);
         std::vector<std::thread> th;
-        for (int q = 0; q < P; ++q) th.emplace_back(pe_main, P, q, std::cref(cases), sh, &ok[(size_t)q]);
+        for (int q = 0; q < P; ++q)
+            th.emplace_back(pe_main, P, q, mode == 1, std::cref(cases), sh, &ok[(size_t)q]);
         for (auto &t : th) t.join();
         for (long v : ok) total += v;
         for (char *h : g_heaps) free(h);
     }
     free(sh);
-    printf("p2p protocol harness: %ld calls OK\n", total);
+    printf("p2p protocol harness: %ld calls OK (host and stream signalling)\n", total);
     return 0;
 }
