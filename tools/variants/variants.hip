@@ -4,8 +4,8 @@
 // product library (sos_amd/libsos_amd.so) contains only the defaults; nothing in it
 // calls or links this file.  fp32 sum only (the headline op):
 //   sosxv_combine : the local combine out = a + b, 20 shapes (0 = the product default)
-//   sosxv_fold    : the 8-input LINEAR fold, 8 shapes (0 = the product default)
-//   sosxv_prefix  : the 2..8-input prefix, 6 shapes (0 = the product default)
+//   sosxv_fold    : the 8-input LINEAR fold, 15 shapes (0 = the product default)
+//   sosxv_prefix  : the 2..8-input prefix, 14 shapes (0 = the product default)
 #include "combine_kernels.h"
 #include "fold_kernels.h"
 
@@ -271,6 +271,84 @@ __global__ __launch_bounds__(kThreads) void k_prefix_lc(PrefixPtrs p, Geom g)
     }
 }
 
+// Buffer-descriptor fold / prefix (round 5): nontemporal loads, stores with explicit aux
+// bits -- sc1 stores leave no line behind in the XCD's L2 (MI355X guide, store flavours),
+// so a 9- or 16-stream kernel's L2 is not filled with written lines whose write-backs
+// interleave with the read streams.  U = 1, one tile per workgroup, same element order.
+template <class T, class OP, int NP, int AUXL, int AUXS>
+__global__ __launch_bounds__(kThreads) void k_fold_buf(T *out, FoldPtrs ins, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    constexpr int kTileBytes = kThreads * 16;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t tb = t * (size_t)kTileBytes;
+        u32x4 x[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            auto r = __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)((const T *)ins.p[k] + g.head) + tb),
+                                                       0, kTileBytes, 0x00020000);
+            x[k] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, 0, AUXL);
+        }
+        auto rO = __builtin_amdgcn_make_buffer_rsrc((void *)((char *)(out + g.head) + tb), 0, kTileBytes,
+                                                    0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(fold_pack<T, OP, NP, SOSX_ORDER_LINEAR>(x), rO,
+                                               (int)threadIdx.x * 16, 0, AUXS);
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)ins.p[k])[i];
+            out[i] = fold_elem<T, OP, NP, SOSX_ORDER_LINEAR>(v);
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
+template <class T, class OP, int NP, int AUXL, int AUXS>
+__global__ __launch_bounds__(kThreads) void k_prefix_buf(PrefixPtrs p, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    constexpr int kTileBytes = kThreads * 16;
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t tb = t * (size_t)kTileBytes;
+        u32x4 x[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            auto r = __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)((const T *)p.in[k] + g.head) + tb),
+                                                       0, kTileBytes, 0x00020000);
+            x[k] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, 0, AUXL);
+        }
+        u32x4 acc = x[0];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            if (k) acc = apply<T, OP>(acc, x[k]);
+            auto rO = __builtin_amdgcn_make_buffer_rsrc((void *)((char *)((T *)p.out[k] + g.head) + tb), 0,
+                                                        kTileBytes, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(acc, rO, (int)threadIdx.x * 16, 0, AUXS);
+        }
+    }
+    if (g.has_rem && blockIdx.x == gridDim.x - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)p.in[k])[i];
+            T acc = v[0];
+            ((T *)p.out[0])[i] = acc;
+#pragma unroll
+            for (int k = 1; k < NP; ++k) {
+                acc = OP::f(acc, v[k]);
+                ((T *)p.out[k])[i] = acc;
+            }
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
 }  // namespace sos
 
 using namespace sos;
@@ -372,6 +450,15 @@ int fold_u_lds(T *out, const FoldPtrs &ins, size_t n, hipStream_t st, unsigned l
     return hip_ok(hipGetLastError());
 }
 
+template <int AUXL, int AUXS>
+int fold_buf(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(T), 1);
+    hipLaunchKernelGGL((k_fold_buf<T, OP, 8, AUXL, AUXS>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st,
+                       out, ins, g);
+    return hip_ok(hipGetLastError());
+}
+
 template <int U>
 int fold_lc(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 {
@@ -382,13 +469,14 @@ int fold_lc(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 }
 
 const char *const kFoldNames[] = {"u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd",
-                                  "lc2", "lc4", "u1_occ4", "u1_occ2", "u2_occ4"};
-constexpr int kNumFold = 13;
+                                  "lc2", "lc4", "u1_occ4", "u1_occ2", "u2_occ4", "buf_nt_st_sc1",
+                                  "buf_nt_st_nt"};
+constexpr int kNumFold = 15;
 
 const char *const kPrefixNames[] = {"u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain", "u8_nt",
                                     "split2_nt", "split2_seed_plain", "lc2", "lc4", "u1_occ4",
-                                    "u1_occ2"};
-constexpr int kNumPrefix = 12;
+                                    "u1_occ2", "buf_nt_st_sc1", "buf_nt_st_nt"};
+constexpr int kNumPrefix = 14;
 
 // Continuation of a prefix from a seed vector: out[k] = seed OP in[0] OP ... OP in[k],
 // left to right, so the second half of a split prefix is bit-identical to the fused one
@@ -469,6 +557,15 @@ int prefix_lc(const PrefixPtrs &p, size_t n, hipStream_t st)
     return hip_ok(hipGetLastError());
 }
 
+template <int NP, int AUXL, int AUXS>
+int prefix_buf(const PrefixPtrs &p, size_t n, hipStream_t st)
+{
+    Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), 1);
+    hipLaunchKernelGGL((k_prefix_buf<T, OP, NP, AUXL, AUXS>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0,
+                       st, p, g);
+    return hip_ok(hipGetLastError());
+}
+
 template <int NP>
 int prefix_lds(const PrefixPtrs &p, size_t n, hipStream_t st, unsigned lds)
 {
@@ -486,6 +583,8 @@ int prefix_np(int v, const PrefixPtrs &p, size_t n, hipStream_t st)
         case 9: return prefix_lc<NP, 4>(p, n, st);
         case 10: return prefix_lds<NP>(p, n, st, 40 << 10);
         case 11: return prefix_lds<NP>(p, n, st, 64 << 10);
+        case 12: return prefix_buf<NP, 2, 16>(p, n, st);
+        case 13: return prefix_buf<NP, 2, 2>(p, n, st);
         case 0: return prefix_u<NP, 1, true>(p, n, st);
         case 1: return prefix_u<NP, 2, true>(p, n, st);
         case 2: return prefix_u<NP, 4, true>(p, n, st);
@@ -583,6 +682,8 @@ int sosxv_fold(int v, float *out, const void *const *ins, size_t n, void *stream
         case 10: return fold_u_lds<8, 1>(out, fp, n, st, 40 << 10);
         case 11: return fold_u_lds<8, 1>(out, fp, n, st, 64 << 10);
         case 12: return fold_u_lds<8, 2>(out, fp, n, st, 40 << 10);
+        case 13: return fold_buf<2, 16>(out, fp, n, st);
+        case 14: return fold_buf<2, 2>(out, fp, n, st);
     }
     return SOSX_ERR_ARG;
 }
