@@ -26,6 +26,18 @@ __global__ __launch_bounds__(kThreads) void k_fold_dyn(T *out, FoldPtrs ins, int
     const size_t stride = (size_t)gridDim.x * kThreads;
     int p2 = 1;
     while (p2 * 2 <= np) p2 *= 2;
+    if (np <= 8) {
+        // one PE's node (the latency-bound small folds): every input's element is loaded
+        // before the first combine, so the P loads are in flight together instead of one
+        // round trip per input (fold_runtime_np_elem: the same operation order)
+        FoldRealignArgs a;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a.p[k] = ins.p[k];
+        a.np = np;
+        for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
+            out[i] = fold_runtime_np_elem<T, OP, ORDER>(a, i);
+        return;
+    }
     for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
         if constexpr (ORDER == SOSX_ORDER_LINEAR) {
             T acc = ((const T *)ins.p[0])[i];

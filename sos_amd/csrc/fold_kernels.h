@@ -140,6 +140,7 @@ __device__ __forceinline__ T fold_runtime_np_elem(const FoldRealignArgs &a, size
     T v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = k < a.np ? ((const T *)a.p[k])[i] : T();
+    // (LINEAR: v[0] OP v[1] OP ...; TREE: fold_elem's recdbl_sw tree, 2 <= np <= 8)
     if constexpr (ORDER == SOSX_ORDER_LINEAR) {
         T acc = v[0];
         for (int k = 1; k < a.np; ++k) acc = OP::f(acc, v[k]);

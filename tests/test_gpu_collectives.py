@@ -127,6 +127,28 @@ def test_fold_runtime_p(torch_cuda, P, order, dt, op):
     assert np.array_equal(bits(from_dev(out, ref)), bits(ref))
 
 
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("dt,op", [(23, 5), (24, 4), (11, 2), (27, 6), (26, 5), (3, 3)])
+def test_fold_small_inputs(torch_cuda, P, order, dt, op):
+    """Folds of inputs of at most 64 KiB each (k_fold_dyn, the latency-bound path of the
+    small team calls): every input's element is loaded before the first combine; the
+    operation order is the plan's, bit for bit against the plan simulator's fold, ragged
+    sizes and an element-misaligned start."""
+    torch = torch_cuda
+    es = O.lib().oracle_type_size(dt)
+    for n in (1, 7, 1000, (1 << 16) // es):
+        ins = [O.fill(dt, 1 if op == 6 else 0, 17, k, n) for k in range(P)]
+        ref = plansim.fold_values(op, dt, ins, order)
+        for off in (0, es if es < 16 else 0):
+            di = [to_dev(torch, a, off) for a in ins]
+            out = torch.zeros_like(to_dev(torch, ins[0], off))
+            _lib.fold(op, dt, order, out.data_ptr() + off, [t.data_ptr() + off for t in di], n)
+            torch.cuda.synchronize()
+            got = from_dev(out, ref, off) if off else from_dev(out, ref)
+            assert np.array_equal(bits(got), bits(ref)), (n, off)
+
+
 @pytest.mark.parametrize("P", [2, 3, 5, 6, 7, 8])
 @pytest.mark.parametrize("dt,op", [(23, 5), (18, 5), (3, 2), (24, 6), (11, 4), (26, 5)])
 @pytest.mark.parametrize("layout", ["own", "peers", "mixed"])

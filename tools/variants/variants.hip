@@ -4,8 +4,8 @@
 // product library (sos_amd/libsos_amd.so) contains only the defaults; nothing in it
 // calls or links this file.  fp32 sum only (the headline op):
 //   sosxv_combine : the local combine out = a + b, 20 shapes (0 = the product default)
-//   sosxv_fold    : the 8-input LINEAR fold, 15 shapes (0 = the product default)
-//   sosxv_prefix  : the 2..8-input prefix, 14 shapes (0 = the product default)
+//   sosxv_fold    : the 8-input LINEAR fold, 18 shapes (0 = the product default)
+//   sosxv_prefix  : the 2..8-input prefix, 16 shapes (0 = the product default)
 #include "combine_kernels.h"
 #include "fold_kernels.h"
 
@@ -451,10 +451,10 @@ int fold_u_lds(T *out, const FoldPtrs &ins, size_t n, hipStream_t st, unsigned l
 }
 
 template <int AUXL, int AUXS>
-int fold_buf(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
+int fold_buf(T *out, const FoldPtrs &ins, size_t n, hipStream_t st, unsigned lds = 0)
 {
     Geom g = make_geom((uintptr_t)out, n, sizeof(T), 1);
-    hipLaunchKernelGGL((k_fold_buf<T, OP, 8, AUXL, AUXS>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st,
+    hipLaunchKernelGGL((k_fold_buf<T, OP, 8, AUXL, AUXS>), dim3(grid_for(g, kNoCap)), dim3(kThreads), lds, st,
                        out, ins, g);
     return hip_ok(hipGetLastError());
 }
@@ -470,13 +470,14 @@ int fold_lc(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 
 const char *const kFoldNames[] = {"u1", "u2", "u4", "st4", "st16", "xcd", "st4_pf", "st16_pf_xcd",
                                   "lc2", "lc4", "u1_occ4", "u1_occ2", "u2_occ4", "buf_nt_st_sc1",
-                                  "buf_nt_st_nt"};
-constexpr int kNumFold = 15;
+                                  "buf_nt_st_nt", "buf_sc1_occ4", "buf_sc1_occ2", "u1_occ3"};
+constexpr int kNumFold = 18;
 
 const char *const kPrefixNames[] = {"u1_nt", "u2_nt", "u4_nt", "u1_plain", "u2_plain", "u8_nt",
                                     "split2_nt", "split2_seed_plain", "lc2", "lc4", "u1_occ4",
-                                    "u1_occ2", "buf_nt_st_sc1", "buf_nt_st_nt"};
-constexpr int kNumPrefix = 14;
+                                    "u1_occ2", "buf_nt_st_sc1", "buf_nt_st_nt", "u1_occ3",
+                                    "buf_sc1_occ2"};
+constexpr int kNumPrefix = 16;
 
 // Continuation of a prefix from a seed vector: out[k] = seed OP in[0] OP ... OP in[k],
 // left to right, so the second half of a split prefix is bit-identical to the fused one
@@ -558,10 +559,10 @@ int prefix_lc(const PrefixPtrs &p, size_t n, hipStream_t st)
 }
 
 template <int NP, int AUXL, int AUXS>
-int prefix_buf(const PrefixPtrs &p, size_t n, hipStream_t st)
+int prefix_buf(const PrefixPtrs &p, size_t n, hipStream_t st, unsigned lds = 0)
 {
     Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), 1);
-    hipLaunchKernelGGL((k_prefix_buf<T, OP, NP, AUXL, AUXS>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0,
+    hipLaunchKernelGGL((k_prefix_buf<T, OP, NP, AUXL, AUXS>), dim3(grid_for(g, kNoCap)), dim3(kThreads), lds,
                        st, p, g);
     return hip_ok(hipGetLastError());
 }
@@ -585,6 +586,8 @@ int prefix_np(int v, const PrefixPtrs &p, size_t n, hipStream_t st)
         case 11: return prefix_lds<NP>(p, n, st, 64 << 10);
         case 12: return prefix_buf<NP, 2, 16>(p, n, st);
         case 13: return prefix_buf<NP, 2, 2>(p, n, st);
+        case 14: return prefix_lds<NP>(p, n, st, 48 << 10);
+        case 15: return prefix_buf<NP, 2, 16>(p, n, st, 64 << 10);
         case 0: return prefix_u<NP, 1, true>(p, n, st);
         case 1: return prefix_u<NP, 2, true>(p, n, st);
         case 2: return prefix_u<NP, 4, true>(p, n, st);
@@ -684,6 +687,9 @@ int sosxv_fold(int v, float *out, const void *const *ins, size_t n, void *stream
         case 12: return fold_u_lds<8, 2>(out, fp, n, st, 40 << 10);
         case 13: return fold_buf<2, 16>(out, fp, n, st);
         case 14: return fold_buf<2, 2>(out, fp, n, st);
+        case 15: return fold_buf<2, 16>(out, fp, n, st, 40 << 10);
+        case 16: return fold_buf<2, 16>(out, fp, n, st, 64 << 10);
+        case 17: return fold_u_lds<8, 1>(out, fp, n, st, 48 << 10);
     }
     return SOSX_ERR_ARG;
 }
