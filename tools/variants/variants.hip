@@ -380,14 +380,18 @@ const char *const kCombineNames[] = {
     "x512_xcd",          // 18
     "x256",              // 19: the k_combine3_x control (same shape as u1_nt)
     "u1_nt_hoist",       // 20: u1_nt with gridDim read once before the tile loop
+    "u1_nt_occ4",        // 21: u1_nt, 40 KiB of unused dynamic LDS: at most 4 workgroups per CU
+    "u1_nt_occ3",        // 22: 48 KiB: at most 3 per CU
+    "u1_nt_occ2",        // 23: 64 KiB: at most 2 per CU
+    "u2_nt_occ4",        // 24
 };
 constexpr int kNumCombine = (int)(sizeof(kCombineNames) / sizeof(kCombineNames[0]));
 
 template <int U, bool NTL, bool NTS>
-int combine_vec(T *out, const T *a, const T *b, size_t n, hipStream_t st, size_t cap)
+int combine_vec(T *out, const T *a, const T *b, size_t n, hipStream_t st, size_t cap, unsigned lds = 0)
 {
     Geom g = make_geom((uintptr_t)out, n, sizeof(T), U);
-    hipLaunchKernelGGL((k_combine3<T, OP, U, NTL, NTS>), dim3(grid_for(g, cap)), dim3(kThreads), 0,
+    hipLaunchKernelGGL((k_combine3<T, OP, U, NTL, NTS>), dim3(grid_for(g, cap)), dim3(kThreads), lds,
                        st, out, a, b, g);
     return hip_ok(hipGetLastError());
 }
@@ -654,6 +658,10 @@ int sosxv_combine(int v, float *out, const float *a, const float *b, size_t n, v
                                out, a, b, g);
             return hip_ok(hipGetLastError());
         }
+        case 21: return combine_vec<1, true, true>(out, a, b, n, st, kNoCap, 40 << 10);
+        case 22: return combine_vec<1, true, true>(out, a, b, n, st, kNoCap, 48 << 10);
+        case 23: return combine_vec<1, true, true>(out, a, b, n, st, kNoCap, 64 << 10);
+        case 24: return combine_vec<2, true, true>(out, a, b, n, st, kNoCap, 40 << 10);
     }
     return SOSX_ERR_ARG;
 }
