@@ -118,6 +118,23 @@ namespace {
 // flight at once instead of one workgroup's; latency, not bandwidth, bounds these calls.
 constexpr size_t kSpreadBytes = 64 * 1024;
 
+// Occupancy cap of the multi-stream streaming kernels (round 5): a
+// fold or prefix reads/writes `streams` concurrent HBM streams, and with every CU full
+// (8 workgroups) the chip holds ~2048 tiles x streams open DRAM rows at once.  Reserving
+// unused dynamic LDS caps the workgroups per CU (160 KiB / bytes): fewer rows open, better
+// row-buffer locality.  Interleaved A/Bs over 9 random buffer layouts, twice
+// (profiles/r5_multistream_ab.json): the 8-input fold (9 streams) 6.10-6.14 -> 6.29-6.35
+// TB/s at 3 per CU; the 8-input prefix (16 streams) 5.75-5.87 -> 5.96-6.07 at 2 per CU;
+// the 4- and 2-input prefixes (8, 4 streams) +2.5 / +1.7 % at 3 per CU.  The 3-stream
+// combine loses with any cap (6.61 -> 6.31 TB/s at 3 per CU), so it has none, and neither
+// do the folds of 2-4 inputs (U > 1 vectors per lane; unmeasured with a cap).
+inline unsigned occupancy_lds(int streams)
+{
+    if (streams >= 12) return 64u << 10;  // 2 workgroups per CU
+    if (streams >= 4) return 48u << 10;   // 3 per CU
+    return 0;
+}
+
 template <class T, class OP, int ORDER>
 int launch_fold_dyn(T *out, const FoldPtrs &ins, int np, size_t n, hipStream_t st)
 {
@@ -141,8 +158,8 @@ int launch_fold_realign(T *out, const FoldPtrs &ins, int np, size_t n, hipStream
         a.p[k] = ins.p[k];
         a.d[k] = (unsigned)((uintptr_t)((const T *)ins.p[k] + g.head) & 15);
     }
-    hipLaunchKernelGGL((k_fold_realign<T, OP, ORDER>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st,
-                       out, a, g);
+    hipLaunchKernelGGL((k_fold_realign<T, OP, ORDER>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
+                       np >= 5 ? occupancy_lds(np + 1) : 0u, st, out, a, g);
     return hip_ok(hipGetLastError());
 }
 
@@ -165,7 +182,7 @@ int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
     constexpr int U = NP <= 2 ? 4 : (NP <= 4 ? 2 : 1);
     Geom g = make_geom(o, n, sizeof(T), U);
     hipLaunchKernelGGL((k_fold<T, OP, NP, ORDER, U>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
-                       0, st, out, ins, g);
+                       U == 1 ? occupancy_lds(NP + 1) : 0u, st, out, ins, g);
     return hip_ok(hipGetLastError());
 }
 
@@ -198,7 +215,7 @@ int launch_prefix_np(const PrefixPtrs &p, size_t n, hipStream_t st)
 {
     Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), kPrefixU);
     hipLaunchKernelGGL((k_prefix<T, OP, NP, kPrefixU, true>), dim3(grid_for(g, kNoCap)),
-                       dim3(kThreads), 0, st, p, g);
+                       dim3(kThreads), occupancy_lds(2 * NP), st, p, g);
     return hip_ok(hipGetLastError());
 }
 
@@ -229,8 +246,8 @@ struct PrefixFn {
                         a.out[k] = p->out[k];
                         a.d[k] = (unsigned)((uintptr_t)((const T *)p->in[k] + g.head) & 15);
                     }
-                    hipLaunchKernelGGL((k_prefix_realign<T, OP>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0,
-                                       st, a, g);
+                    hipLaunchKernelGGL((k_prefix_realign<T, OP>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
+                                       occupancy_lds(2 * np), st, a, g);
                     return hip_ok(hipGetLastError());
                 }
             }
