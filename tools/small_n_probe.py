@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--sizes", default="1,131072,1048576")
+    ap.add_argument("--rounds", type=int, default=7)
     a = ap.parse_args()
     import torch
     import variants as V
@@ -54,25 +55,31 @@ def main():
                                                  [y + k * fold_n * 4 for k in range(8)], fold_n, S),
         }
         row = {}
-        for name, fn in shapes.items():
-            for i in range(5):
-                fn(*bufs[i % npairs])
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            e0.record(stream)
-            for i in range(a.reps):
-                fn(*bufs[i % npairs])
-            e1.record(stream)
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / a.reps
+        times = {name: [] for name in shapes}
+        for rnd in range(a.rounds):      # shapes interleaved, a median over rounds
+            for name, fn in shapes.items():
+                for i in range(5):
+                    fn(*bufs[i % npairs])
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record(stream)
+                for i in range(a.reps):
+                    fn(*bufs[(i + rnd) % npairs])
+                e1.record(stream)
+                torch.cuda.synchronize()
+                times[name].append(e0.elapsed_time(e1) * 1e3 / a.reps)
+        for name in shapes:
+            us = sorted(times[name])[len(times[name]) // 2]
             algo = 3 * nb if "combine" in name else 9 * fold_n * 4
-            row[name] = {"us_per_launch": round(us, 3), "GBs": round(algo / (us * 1e-6) / 1e9, 1)}
+            row[name] = {"us_per_launch_median": round(us, 3), "us_range": [round(min(times[name]), 3),
+                                                                           round(max(times[name]), 3)],
+                         "GBs": round(algo / (us * 1e-6) / 1e9, 1)}
             print(f"n={n:>9} {name:>20} {us:8.3f} us {row[name]['GBs']:9.1f} GB/s", file=sys.stderr, flush=True)
         out[str(n)] = row
         for x, y in bufs:
             SH.lib().shmemx_free_device(x)
             SH.lib().shmemx_free_device(y)
-    print(json.dumps({"small_n": out, "reps": a.reps,
+    print(json.dumps({"small_n": out, "reps": a.reps, "rounds": a.rounds,
                       "ideal_us_1Mi_combine_at_6p6TBs": round(12 * 2**20 / 6.6e12 * 1e6, 3)}))
     SH.shmem_finalize()
 
