@@ -76,6 +76,7 @@ struct Sig {
     char *dbase = nullptr;          // device view of the shared segment
     long long limit_ticks = 0;      // device wall-clock ticks of SHMEMX_P2P_TIMEOUT
     sosp2p::StreamLocal sl;         // pair counters and descriptor indices (cumulative)
+    bool host_entry = true;         // SHMEMX_P2P_ENTRY: the entry boundary on the host
 };
 Sig g_sig;
 
@@ -325,6 +326,10 @@ void p2p_signal_setup()
     const char *e = getenv("SHMEMX_P2P_SIGNAL");
     const bool want = e && *e ? strcmp(e, "host") != 0 : one_device;
     g_sig.on = g_sig.capable && want;
+    // SHMEMX_P2P_ENTRY = host | device: where stream mode runs the call's entry boundary
+    // (either mode interoperates with the other: the same counters, the same values)
+    const char *en = getenv("SHMEMX_P2P_ENTRY");
+    g_sig.host_entry = !(en && strcmp(en, "device") == 0);
     debug_msg("p2p transport signalling: %s (stream mode %s; PEs on %s)", g_sig.on ? "stream" : "host",
               g_sig.capable ? "available" : "unavailable", one_device ? "one device" : "several devices");
 }
@@ -411,6 +416,7 @@ struct HipBackend {
     void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what) { spin_until(a, want, what); }
     void spin_u64(const uint64_t *a, uint64_t want, const char *what) { spin_until_u64(a, want, what); }
     void entry_hook() { stall_hook(); }
+    bool host_entry() { return g_sig.host_entry; }
     bool device_wait_failed()
     {
         if (__atomic_load_n(&shared()->sig_err[my_world], __ATOMIC_ACQUIRE))

@@ -256,7 +256,8 @@ int exec_host(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of,
 // at once.  The call's offsets travel ahead through a descriptor ring per ordered pair
 // (host handshake, never waiting on a GPU); between rounds the pair counters move in
 // stream order (a signal step: stores, then bounded waits), carried by a small gather's
-// own launch when it can; the call's entry and exit boundaries run on the host.
+// own launch when it can; the call's exit boundary runs on the host, its entry boundary
+// on the host or (host_entry() false) as the first queued step.
 // Backend B adds to exec_host's:
 //   int release()                     a system-scope release in stream order
 //   int signal(nw, waddr, wval, nq, qaddr, qval)              one queued step
@@ -264,6 +265,7 @@ int exec_host(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of,
 //   uint64_t *dev(uint64_t *), const uint64_t *dev(const uint64_t *)   the step's view
 //   void spin_u64(const uint64_t *a, uint64_t want, const char *what)  host wait
 //   void entry_hook()                 after the entry boundary (test hook)
+//   bool host_entry()                 entry boundary on the host (else queued)
 //   bool device_wait_failed()         a queued wait timed out (after complete())
 template <class B, class WorldOf>
 int exec_stream(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of, int alg,
@@ -359,9 +361,16 @@ int exec_stream(const sosplan::Plan &plan, int P, int me, const WorldOf &world_o
         }
         int rc;
         bool step_pending = false;  // the signalling step still to be enqueued
-        if (first_xfer_round) {
-            // the entry boundary runs on the host: nothing is queued ahead of it that a
-            // signal step could overlap (complete only when this round sends)
+        if (first_xfer_round && !be.host_entry()) {
+            // device entry: the first round's posts and waits are a signalling step in
+            // stream order like every later round's (a system-scope release ahead of the
+            // posts), so the call waits for the GPU once, at its end
+            first_xfer_round = false;
+            be.entry_hook();
+            step_pending = true;
+        } else if (first_xfer_round) {
+            // host entry: the boundary runs on the host (complete only when this round
+            // sends), then the host posts and waits
             first_xfer_round = false;
             bool sends = false;
             for (const auto &x : r.xfers) sends |= x.send != 0;

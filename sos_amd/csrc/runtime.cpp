@@ -488,10 +488,21 @@ hipError_t release_system(hipStream_t stream)
     return hipEventRecord(s.sys_ev, stream);
 }
 
+// The release event, then a stream synchronisation: it waits for the event too, and
+// costs what a plain hipStreamSynchronize does, 1.5-4.5 us less per call than waiting on
+// the event itself (profiles/r5_sync_cost.json).  Test build only: SOSX_TEST_EVENT_WAIT=1
+// waits with hipEventSynchronize, as round 5 first did (the A/B of DESIGN.md section 6.2).
 hipError_t sync_system(hipStream_t stream)
 {
     hipError_t e = release_system(stream);
-    if (e == hipSuccess) e = hipEventSynchronize(st().sys_ev);
+#ifdef SOSX_TEST_HOOKS
+    static const bool event_wait = [] {
+        const char *v = getenv("SOSX_TEST_EVENT_WAIT");
+        return v && *v == '1';
+    }();
+    if (event_wait) return e == hipSuccess ? hipEventSynchronize(st().sys_ev) : e;
+#endif
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
     return e;
 }
 

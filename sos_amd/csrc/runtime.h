@@ -147,7 +147,7 @@ void hip_check(hipError_t e, const char *what);
 void nccl_check(ncclResult_t r, const char *what);
 
 // Completion with a SYSTEM-scope release: record an event created with
-// hipEventReleaseToSystem on `stream` and wait for it.  The marker's release writes every
+// hipEventReleaseToSystem on `stream` and wait for the stream (which waits for it).  The marker's release writes every
 // XCD's L2 back to memory, so what the stream's kernels stored is in HBM when this
 // returns: visible to DMA reads (hipMemcpy on any stream, the host), to peer GPUs reading
 // over xGMI and to other processes.  A plain hipStreamSynchronize only promises the

@@ -17,6 +17,8 @@
 // Build with -DBROKEN_DRAIN to drop the drain before a round's receives are marked
 // consumed (step 4): the sanitizer must then report the race (the negative control).
 //
+// Stream mode runs with the entry boundary on the host, queued, and mixed across PEs.
+//
 // Usage: p2p_proto_harness [iters]     prints "p2p protocol harness: N calls OK", exit 0
 #include <stdio.h>
 #include <stdlib.h>
@@ -97,6 +99,7 @@ constexpr size_t kHeap = 8u << 20;
 
 struct CpuBackend {
     Stream *s;
+    bool entry_on_host;
     int complete()
     {
         s->drain();
@@ -202,6 +205,7 @@ struct CpuBackend {
         }
     }
     void entry_hook() {}
+    bool host_entry() { return entry_on_host; }
     bool device_wait_failed() { return false; }
     const char *peer_base(int pw) { return g_heaps[(size_t)pw]; }
     void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what)
@@ -233,11 +237,14 @@ struct Case {
 };
 
 // One PE: `cases` calls in order, every result checked.
-void pe_main(int P, int me, bool stream_mode, const std::vector<Case> &cases, sosp2p::Shared *sh,
+// mode 0: host signalling; stream signalling with the entry boundary 1: on the host,
+// 2: queued, 3: queued on odd PEs only (the two interoperate)
+void pe_main(int P, int me, int mode, const std::vector<Case> &cases, sosp2p::Shared *sh,
              long *ok_calls)
 {
     Stream st;
-    CpuBackend be{&st};
+    const bool stream_mode = mode > 0;
+    CpuBackend be{&st, mode == 1 || (mode == 3 && me % 2 == 0)};
     sosp2p::Local loc;
     sosp2p::StreamLocal sl;
     char *heap = g_heaps[(size_t)me];
@@ -308,7 +315,7 @@ int main(int argc, char **argv)
     auto *sh = (sosp2p::Shared *)calloc(1, sizeof(sosp2p::Shared));
     const int algs[] = {SOSX_ALG_RING, SOSX_ALG_RECDBL, SOSX_ALG_RECHALVING, SOSX_ALG_RECDBL_DIRECT,
                         SOSX_ALG_RECDBL_GATHER, SOSX_PLAN_INSCAN, SOSX_PLAN_EXSCAN};
-    for (int mode = 0; mode < 2; ++mode)
+    for (int mode = 0; mode < 4; ++mode)
     for (int P : {2, 3, 4, 5, 8, 12}) {
         g_heaps.clear();
         for (int q = 0; q < P; ++q) {
@@ -332,12 +339,12 @@ int main(int argc, char **argv)
         std::vector<long> ok((size_t)P, 0);
         std::vector<std::thread> th;
         for (int q = 0; q < P; ++q)
-            th.emplace_back(pe_main, P, q, mode == 1, std::cref(cases), sh, &ok[(size_t)q]);
+            th.emplace_back(pe_main, P, q, mode, std::cref(cases), sh, &ok[(size_t)q]);
         for (auto &t : th) t.join();
         for (long v : ok) total += v;
         for (char *h : g_heaps) free(h);
     }
     free(sh);
-    printf("p2p protocol harness: %ld calls OK (host and stream signalling)\n", total);
+    printf("p2p protocol harness: %ld calls OK (host and stream signalling, both entries)\n", total);
     return 0;
 }

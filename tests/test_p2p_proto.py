@@ -41,7 +41,7 @@ def test_host_protocol_race_free(harness):
     r = subprocess.run([harness, "1"], capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
-    assert "calls OK" in r.stdout and int(r.stdout.split(":")[1].split()[0]) > 4000, r.stdout
+    assert "calls OK" in r.stdout and int(r.stdout.split(":")[1].split()[0]) > 8000, r.stdout
 
 
 def test_broken_protocol_is_caught():
