@@ -94,45 +94,28 @@ __global__ __launch_bounds__(kThreads) void k_fold(T *out, FoldPtrs ins, Geom g)
 }
 
 // ---------------------------------------------------------------------------------
-// The P-way fold (2 <= P <= 8, at run time) when some inputs are NOT 16-B congruent with
-// the output: a team reduction whose source and target sit at different 16-B offsets
-// (the PE's own source chunk, or the peers' sources read in place, against exchange
-// scratch congruent with the target).  16-B vectors throughout: an input at byte offset
-// d[k] != 0 is read as the two aligned vectors its bytes straddle and funnel-shifted
-// into place (realign16; see k_combine3_realign for why the extra bytes are safe to
-// load).  LINEAR: acc = in[0] OP in[1] OP ... (the ring); TREE: the recdbl_sw tree of
-// fold_elem (the extras folded into the first P - p2 leaves, then distance 1, 2, 4 pairs,
-// the lower subtree the left operand) -- with P at run time on compile-time indices, so
-// one kernel per (type, op, order) serves every P.
+// The P-way fold (2 <= P <= 8) when some inputs are NOT 16-B congruent with the output: a
+// team reduction whose source and target sit at different 16-B offsets (the PE's own
+// source chunk, or the peers' sources read in place, against exchange scratch congruent
+// with the target).  16-B vectors throughout, two shapes:
+//   k_fold_realign_np  inputs at different offsets: an input at byte offset d[k] != 0 is
+//                      read as the two aligned vectors its bytes straddle and
+//                      funnel-shifted into place (realign16; see k_combine3_realign for
+//                      why the extra bytes are safe to load);
+//   k_fold_outshift    every input at one offset: fold in the inputs' frame, realign the
+//                      output.
+// LINEAR: acc = in[0] OP in[1] OP ... (the ring); TREE: the recdbl_sw tree of fold_elem
+// (the extras folded into the first P - p2 leaves, then distance 1, 2, 4 pairs, the lower
+// subtree the left operand).  The ragged head and tail use the runtime-P element fold.
+// Round 5 (profiles/r5_fold_outshift.txt): both with P at compile time and no occupancy
+// cap; the runtime-P vector kernel they replace branched per input between its loads
+// (3.2-3.8 TB/s with every input incongruent, 5.7 with one).
 // ---------------------------------------------------------------------------------
 struct FoldRealignArgs {
     const void *p[8];
     unsigned d[8];
     int np;
 };
-
-template <class T, class OP, int ORDER>
-__device__ __forceinline__ u32x4 fold_runtime_np(u32x4 (&x)[8], int np)
-{
-    if constexpr (ORDER == SOSX_ORDER_LINEAR) {
-        u32x4 acc = x[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k)
-            if (k < np) acc = apply<T, OP>(acc, x[k]);
-        return acc;
-    } else {
-        const int p2 = np >= 8 ? 8 : np >= 4 ? 4 : 2;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (k < np - p2) x[k] = apply<T, OP>(x[k], x[k + p2]);
-#pragma unroll
-        for (int d = 1; d < 8; d <<= 1)
-#pragma unroll
-            for (int k = 0; k < 8; k += 2 * d)
-                if (d < p2 && k < p2) x[k] = apply<T, OP>(x[k], x[k + d]);
-        return x[0];
-    }
-}
 
 template <class T, class OP, int ORDER>
 __device__ __forceinline__ T fold_runtime_np_elem(const FoldRealignArgs &a, size_t i)
@@ -159,27 +142,30 @@ __device__ __forceinline__ T fold_runtime_np_elem(const FoldRealignArgs &a, size
     }
 }
 
-template <class T, class OP, int ORDER = SOSX_ORDER_LINEAR>
-__global__ __launch_bounds__(kThreads) void k_fold_realign(T *out, FoldRealignArgs a, Geom g)
+// Inputs at different offsets: every input's aligned vector is loaded first, then the
+// second vector of each incongruent input, then the fold.
+template <class T, class OP, int NP, int ORDER>
+__global__ __launch_bounds__(kThreads) void k_fold_realign_np(T *out, FoldRealignArgs a, Geom g)
 {
     constexpr int V = Pack<T>::N;
     const size_t nblk = gridDim.x;
-    const int np = a.np;
     u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    const u32x4 *I[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+        I[k] = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>((const T *)a.p[k] + g.head) - a.d[k]);
     for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
         const size_t i = t * (size_t)kThreads + threadIdx.x;
-        u32x4 x[8];
+        u32x4 x[NP], y[NP];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (k < np) {
-                const unsigned d = a.d[k];
-                const u32x4 *I = reinterpret_cast<const u32x4 *>(
-                    reinterpret_cast<const char *>((const T *)a.p[k] + g.head) - d);
-                const u32x4 lo = ldv<true>(I + i);
-                x[k] = d ? realign16(lo, ldv<true>(I + i + 1), d) : lo;
-            }
-        }
-        stv<true>(O + i, fold_runtime_np<T, OP, ORDER>(x, np));
+        for (int k = 0; k < NP; ++k) x[k] = ldv<true>(I[k] + i);
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            if (a.d[k]) x[k] = realign16(x[k], y[k], a.d[k]);
+        stv<true>(O + i, fold_pack<T, OP, NP, ORDER>(x));
     }
     if (g.has_rem && blockIdx.x == nblk - 1) {
         for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = fold_runtime_np_elem<T, OP, ORDER>(a, i);
@@ -187,6 +173,69 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign(T *out, FoldRealignAr
             out[i] = fold_runtime_np_elem<T, OP, ORDER>(a, i);
     }
 }
+
+// Every input at the SAME 16-B offset d != 0 from the output (the inputs congruent with
+// one another: the p2p ring's in-place fold of the peers' sources when source and target
+// sit at different offsets in the symmetric heap).  Fold in the inputs' frame, one vector
+// per input per lane, and realign the OUTPUT: out vector i = realign16(F_i, F_i+1, d),
+// F_i+1 taken from the next lane; the last lane of each wave folds its F_i+1 itself
+// (k_fold_realign_np would load two vectors per input: 4.2-4.4 TB/s here, 5.8-6.1 this way).
+template <class T, class OP, int NP, int ORDER>
+__global__ __launch_bounds__(kThreads) void k_fold_outshift(T *out, FoldRealignArgs a, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    const size_t nblk = gridDim.x;
+    const unsigned d = a.d[0];
+    const bool last_lane = (threadIdx.x & 63) == 63;
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    const u32x4 *I[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+        I[k] = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>((const T *)a.p[k] + g.head) - d);
+    for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        u32x4 x[NP], y[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) x[k] = ldv<true>(I[k] + i);
+        if (last_lane) {  // its F_i+1 belongs to the next wave (or workgroup)
+#pragma unroll
+            for (int k = 0; k < NP; ++k) y[k] = ldv<true>(I[k] + i + 1);
+        }
+        const u32x4 f = fold_pack<T, OP, NP, ORDER>(x);
+        u32x4 nx;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) nx[c] = __shfl_down(f[c], 1u);
+        if (last_lane) nx = fold_pack<T, OP, NP, ORDER>(y);
+        stv<true>(O + i, realign16(f, nx, d));
+    }
+    if (g.has_rem && blockIdx.x == nblk - 1) {
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = fold_runtime_np_elem<T, OP, ORDER>(a, i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            out[i] = fold_runtime_np_elem<T, OP, ORDER>(a, i);
+    }
+}
+
+// Occupancy cap of the multi-stream streaming kernels (round 5): a
+// fold or prefix reads/writes `streams` concurrent HBM streams, and with every CU full
+// (8 workgroups) the chip holds ~2048 tiles x streams open DRAM rows at once.  Reserving
+// unused dynamic LDS caps the workgroups per CU (160 KiB / bytes): fewer rows open, better
+// row-buffer locality.  Interleaved A/Bs over 9 random buffer layouts, twice
+// (profiles/r5_multistream_ab.json): the 8-input fold (9 streams) 6.10-6.14 -> 6.29-6.35
+// TB/s at 3 per CU; the 8-input prefix (16 streams) 5.75-5.87 -> 5.96-6.07 at 2 per CU;
+// the 4- and 2-input prefixes (8, 4 streams) +2.5 / +1.7 % at 3 per CU.  The 3-stream
+// combine loses with any cap (6.61 -> 6.31 TB/s at 3 per CU), so it has none, and neither
+// do the folds of 2-4 inputs (U > 1 vectors per lane; unmeasured with a cap).
+inline unsigned occupancy_lds(int streams)
+{
+    if (streams >= 12) return 64u << 10;  // 2 workgroups per CU
+    if (streams >= 4) return 48u << 10;   // 3 per CU
+    return 0;
+}
+
+// The fold of one element order over any (type, op) (fold_order.hip, one object per
+// order); sosx_fold dispatches to them.
+int fold_linear(int op, int dtype, void *out, const FoldPtrs *ins, int nin, size_t n, hipStream_t st);
+int fold_tree(int op, int dtype, void *out, const FoldPtrs *ins, int nin, size_t n, hipStream_t st);
 
 constexpr int kMaxPrefix = 64;
 
@@ -247,7 +296,7 @@ __global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
 // The team scan's prefix (1 <= P <= 8, at run time) when some INPUTS sit at another 16-B
 // offset than the outputs (a scan whose source and target are at different offsets: the
 // PE's own source chunk against target-congruent scratch); the outputs are congruent.
-// Inputs realigned as in k_fold_realign; every input vector of a tile is loaded before
+// Inputs realigned as in k_fold_realign_np; every input vector of a tile is loaded before
 // the first store, as in k_prefix (an output may alias an input: the aliased pair is
 // congruent, so it is never read past its own vector).
 struct PrefixRealignArgs {
@@ -257,48 +306,112 @@ struct PrefixRealignArgs {
     int np;
 };
 
-template <class T, class OP>
-__global__ __launch_bounds__(kThreads) void k_prefix_realign(PrefixRealignArgs a, Geom g)
+// P known at compile time (round 5, as k_fold_realign_np): every input's aligned vector,
+// then the second vector of each incongruent input, then the prefix.  Replaced a
+// runtime-P kernel that branched per input between its loads (profiles/r5_fold_outshift.txt:
+// 8 x 16Mi fp32, input 0 at +4 B 4.06 -> 5.79-5.82 TB/s, every input at +4 3.39 -> 4.57).
+template <class T, class OP, int NP>
+__global__ __launch_bounds__(kThreads) void k_prefix_realign_np(PrefixRealignArgs a, Geom g)
 {
     constexpr int V = Pack<T>::N;
     const size_t nblk = gridDim.x;
-    const int np = a.np;
+    const u32x4 *I[NP];
+    u32x4 *O[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        I[k] = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>((const T *)a.in[k] + g.head) - a.d[k]);
+        O[k] = reinterpret_cast<u32x4 *>((T *)a.out[k] + g.head);
+    }
     for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
         const size_t i = t * (size_t)kThreads + threadIdx.x;
-        u32x4 x[8];
+        u32x4 x[NP], y[NP];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (k < np) {
-                const unsigned d = a.d[k];
-                const u32x4 *I = reinterpret_cast<const u32x4 *>(
-                    reinterpret_cast<const char *>((const T *)a.in[k] + g.head) - d);
-                const u32x4 lo = ldv<true>(I + i);
-                x[k] = d ? realign16(lo, ldv<true>(I + i + 1), d) : lo;
-            }
-        }
+        for (int k = 0; k < NP; ++k) x[k] = ldv<true>(I[k] + i);
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            if (a.d[k]) x[k] = realign16(x[k], y[k], a.d[k]);
         u32x4 acc = x[0];
-        stv<true>(reinterpret_cast<u32x4 *>((T *)a.out[0] + g.head) + i, acc);
+        stv<true>(O[0] + i, acc);
 #pragma unroll
-        for (int k = 1; k < 8; ++k) {
-            if (k < np) {
-                acc = apply<T, OP>(acc, x[k]);
-                stv<true>(reinterpret_cast<u32x4 *>((T *)a.out[k] + g.head) + i, acc);
-            }
+        for (int k = 1; k < NP; ++k) {
+            acc = apply<T, OP>(acc, x[k]);
+            stv<true>(O[k] + i, acc);
         }
     }
     if (g.has_rem && blockIdx.x == nblk - 1) {
         auto one = [&](size_t i) {
-            T v[8];
+            T v[NP];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = k < np ? ((const T *)a.in[k])[i] : T();
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)a.in[k])[i];
             T acc = v[0];
             ((T *)a.out[0])[i] = acc;
 #pragma unroll
-            for (int k = 1; k < 8; ++k) {
-                if (k < np) {
-                    acc = OP::f(acc, v[k]);
-                    ((T *)a.out[k])[i] = acc;
-                }
+            for (int k = 1; k < NP; ++k) {
+                acc = OP::f(acc, v[k]);
+                ((T *)a.out[k])[i] = acc;
+            }
+        };
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            one(i);
+    }
+}
+
+// Every input at the SAME 16-B offset d != 0 from the (congruent) outputs: the prefix in
+// the inputs' frame, each output realigned (k_fold_outshift's scheme, once per output:
+// the next lane's running value by __shfl_down, the last lane of a wave folding the next
+// vector itself).  Aliasing as k_prefix: every load of the tile before the first store.
+template <class T, class OP, int NP>
+__global__ __launch_bounds__(kThreads) void k_prefix_outshift(PrefixRealignArgs a, Geom g)
+{
+    constexpr int V = Pack<T>::N;
+    const size_t nblk = gridDim.x;
+    const unsigned d = a.d[0];
+    const bool last_lane = (threadIdx.x & 63) == 63;
+    const u32x4 *I[NP];
+    u32x4 *O[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        I[k] = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>((const T *)a.in[k] + g.head) - d);
+        O[k] = reinterpret_cast<u32x4 *>((T *)a.out[k] + g.head);
+    }
+    for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        u32x4 x[NP], y[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) x[k] = ldv<true>(I[k] + i);
+        if (last_lane) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) y[k] = ldv<true>(I[k] + i + 1);
+        }
+        u32x4 acc = x[0], accn = y[0];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            if (k > 0) {
+                acc = apply<T, OP>(acc, x[k]);
+                if (last_lane) accn = apply<T, OP>(accn, y[k]);
+            }
+            u32x4 nx;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) nx[c] = __shfl_down(acc[c], 1u);
+            if (last_lane) nx = accn;
+            stv<true>(O[k] + i, realign16(acc, nx, d));
+        }
+    }
+    if (g.has_rem && blockIdx.x == nblk - 1) {
+        auto one = [&](size_t i) {
+            T v[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[k] = ((const T *)a.in[k])[i];
+            T acc = v[0];
+            ((T *)a.out[0])[i] = acc;
+#pragma unroll
+            for (int k = 1; k < NP; ++k) {
+                acc = OP::f(acc, v[k]);
+                ((T *)a.out[k])[i] = acc;
             }
         };
         for (size_t i = threadIdx.x; i < g.head; i += kThreads) one(i);

@@ -73,15 +73,17 @@ def test_prefix_kernel(torch_cuda, np_, dt):
 @pytest.mark.parametrize("dt", [23, 24, 4, 1, 27])
 def test_prefix_realigned_inputs(torch_cuda, np_, dt):
     """SUM prefix whose inputs sit at other 16-B offsets than its (congruent) outputs
-    (k_prefix_realign: a scan with source and target at different offsets), input 0 only
-    or every input at its own offset, ragged sizes; bit for bit against the in-order
-    prefix of the oracle's reduce_local."""
+    (a scan with source and target at different offsets): input 0 only, every input at
+    its own offset (k_prefix_realign_np), every input at one offset (k_prefix_outshift,
+    the outputs realigned), ragged sizes; bit for bit against the in-order prefix of the
+    oracle's reduce_local."""
     torch = torch_cuda
     es = O.lib().oracle_type_size(dt)
     for n in (999, (1 << 18) + 5):
         ins = [src_of(dt, n + 7, k, n) for k in range(np_)]
         ref = cpu_prefix(5, dt, ins)
-        for offs in ([es % 16] + [0] * (np_ - 1), [(es * (k + 1)) % 16 for k in range(np_)]):
+        for offs in ([es % 16] + [0] * (np_ - 1), [(es * (k + 1)) % 16 for k in range(np_)],
+                     [es % 16] * np_):
             di = [to_dev(torch, a, off) for a, off in zip(ins, offs)]
             do = [torch.zeros_like(to_dev(torch, a)) for a in ins]
             _lib.prefix(5, dt, [t.data_ptr() for t in do], [t.data_ptr() + off for t, off in zip(di, offs)], n)
@@ -151,14 +153,15 @@ def test_fold_small_inputs(torch_cuda, P, order, dt, op):
 
 @pytest.mark.parametrize("P", [2, 3, 5, 6, 7, 8])
 @pytest.mark.parametrize("dt,op", [(23, 5), (18, 5), (3, 2), (24, 6), (11, 4), (26, 5)])
-@pytest.mark.parametrize("layout", ["own", "peers", "mixed"])
+@pytest.mark.parametrize("layout", ["own", "peers", "peers_es", "mixed"])
 @pytest.mark.parametrize("order", [0, 1])
 def test_fold_realigned_inputs(torch_cuda, P, dt, op, layout, order):
     """Folds past 64 KiB per input whose inputs sit at other 16-B offsets than the output
     (k_fold_realign), in the ring's LINEAR order and in recdbl_sw's TREE order (the extras
     first, then the pairwise tree): the PE's own source chunk only ("own", the ring at PE
-    me with source and target at different offsets), every input ("peers", the p2p
-    transport's in-place reads of the peers' sources), or each input at its own offset
+    me with source and target at different offsets), every input at one offset ("peers"
+    at +8, "peers_es" at +element size: the p2p transport's in-place reads of the peers'
+    sources, k_fold_outshift realigning the output), or each input at its own offset
     ("mixed"); ragged sizes; bit for bit against the plan simulator's fold."""
     torch = torch_cuda
     es = O.lib().oracle_type_size(dt)
@@ -169,6 +172,8 @@ def test_fold_realigned_inputs(torch_cuda, P, dt, op, layout, order):
             offs = [es] + [0] * (P - 1)
         elif layout == "peers":
             offs = [8 if es <= 8 else 0] * P
+        elif layout == "peers_es":
+            offs = [es % 16] * P
         else:
             offs = [(es * k) % 16 for k in range(1, P + 1)]
         di = [to_dev(torch, a, off) for a, off in zip(ins, offs)]
