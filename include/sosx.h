@@ -256,6 +256,10 @@ int sosx_small_stage(void *dst, const void *src, size_t bytes, uint64_t *const *
 
 long sosx_small_path_calls(void);
 long sosx_small_path_device_calls(void);
+/* The resident small-path executor (SHMEMX_SMALL_RESIDENT=1, sos_amd/csrc/resident.h):
+ * requests it served and kernel launches it took in this process. */
+long sosx_small_resident_calls(void);
+long sosx_small_resident_launches(void);
 /* Limit for device-resident operands on that path: a call takes it when team size *
  * operand bytes <= team_bytes (0: never; default SHMEMX_SMALL_DEVICE, 128 KiB).  Returns
  * the previous limit.  Collective in effect: every PE of a team must hold the same limit

@@ -1,0 +1,55 @@
+// resident.h -- the resident small-collective executor's shared words (smallpath.cpp on
+// the host, k_resident in small.hip on the GPU).
+//
+// A launch + completion wait costs 10-13 us on MI355X whatever the wait primitive
+// (profiles/r5_sync_cost.json); a request/answer round trip through a kernel that stays
+// resident and polls pinned host memory costs 1.7 us (profiles/r5_resident.txt).  With
+// SHMEMX_SMALL_RESIDENT=1 the small shared-memory path's recdbl_sw folds and linear folds
+// (scans, broadcasts) of host operands run on such a kernel: one per (type, op) used,
+// one workgroup, launched on the first request and exiting on its own after
+// SHMEMX_SMALL_RESIDENT_IDLE_US of idleness (default 2000) or at shmem_finalize.
+//
+// Protocol (every word in pinned, coherent host memory):
+//   host  : write the descriptor d, then req = k (release);
+//   kernel: req > last -> copy d (after the acquire), compute, fence at system scope,
+//           done = k (release); exits on stop or idleness, storing exited = 1 last;
+//   host  : wait for done >= k; a kernel seen exited with done < k is relaunched (the new
+//           one reads done at start and takes request k), so a request is never lost to
+//           an idle exit racing the host's post.
+#pragma once
+#include <stdint.h>
+
+#define SOSX_RESIDENT_FOLD 0    /* recdbl_sw tree over np leaves (+ extras): k_small_fold's value */
+#define SOSX_RESIDENT_LINEAR 1  /* in[0] OP in[1] ... OP in[np-1]: k_small_ring's single chunk */
+#define SOSX_RESIDENT_MAX_BYTES (16 * 1024)
+
+struct SosxResidentDesc {
+    uint32_t kind;
+    uint32_t np;                 /* leaves (FOLD: 1, 2, 4, 8) or inputs (LINEAR: 1..8) */
+    uint64_t count;              /* elements, count * size <= SOSX_RESIDENT_MAX_BYTES */
+    void *out;
+    const void *in[8];
+    const void *extra[8];        /* FOLD: null where the leaf has no extra PE */
+    uint32_t vec;                /* every operand 16-B aligned: 16-B vectors per lane */
+    uint32_t pad;
+};
+
+struct SosxResidentCtl {
+    uint64_t req;
+    uint64_t done;
+    uint64_t stop;
+    uint64_t exited;
+    uint64_t pad[4];
+    struct SosxResidentDesc d;
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* Launch the resident executor of (op, dtype) on `stream` over `ctl` (device view of
+ * pinned host memory): one workgroup, until ctl->stop or `idle_ticks` device wall-clock
+ * ticks without a request. */
+int sosx_resident_launch(int op, int dtype, struct SosxResidentCtl *ctl, long long idle_ticks, void *stream);
+#ifdef __cplusplus
+}
+#endif

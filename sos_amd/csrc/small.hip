@@ -14,6 +14,7 @@
 // workgroup then stores the call's sequence number into its own word of pinned host
 // memory, which the host polls.
 #include "fold_kernels.h"
+#include "resident.h"
 
 namespace sos {
 
@@ -90,11 +91,10 @@ __device__ __forceinline__ void store_pack(T *out, size_t i0, const Pack<T> &r, 
 
 // VEC: lane L handles elements [L*V, L*V + V) as 16-B vectors (every leaf/extra 16-B
 // aligned); the last, partial vector goes element by element.  Otherwise one element per
-// lane.
+// lane.  (One lane's share: k_small_fold and the resident executor below.)
 template <class T, class OP, int P2, bool VEC, class A>
-__global__ __launch_bounds__(kThreads) void k_small_fold(T *out, A a, size_t n)
+__device__ __forceinline__ void small_fold_lane(T *out, const A &a, size_t n, size_t lane)
 {
-    const size_t lane = (size_t)blockIdx.x * kThreads + threadIdx.x;
     if constexpr (VEC && P2 > 0) {
         constexpr int V = Pack<T>::N;
         const size_t i0 = lane * V;
@@ -123,6 +123,12 @@ __global__ __launch_bounds__(kThreads) void k_small_fold(T *out, A a, size_t n)
     } else {
         if (lane < n) out[lane] = small_tree_elem<T, OP, P2, A>(a, lane);
     }
+}
+
+template <class T, class OP, int P2, bool VEC, class A>
+__global__ __launch_bounds__(kThreads) void k_small_fold(T *out, A a, size_t n)
+{
+    small_fold_lane<T, OP, P2, VEC, A>(out, a, n, (size_t)blockIdx.x * kThreads + threadIdx.x);
     signal_done(a.flags, a.seq);
 }
 
@@ -252,6 +258,124 @@ __global__ __launch_bounds__(kStageThreads) void k_small_stage(A a)
         __hip_atomic_store(a.word[threadIdx.x], a.val[threadIdx.x], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---------------------------------------------------------------------------------
+// The resident executor (resident.h): one workgroup that stays on the GPU and serves the
+// small path's requests from pinned host memory, so a call costs a request/answer round
+// trip instead of a launch and its completion wait.  Thread 0 polls; the workgroup
+// computes the request as k_small_fold / the single-chunk k_small_ring would, lane by
+// lane, fences at system scope and answers.  Every wave leaves the loop on `stop` or
+// after `idle_ticks` without a request.
+// ---------------------------------------------------------------------------------
+template <class T, class OP>
+__device__ __forceinline__ void resident_fold(const SosxResidentDesc &d)
+{
+    SmallFoldArgsT<8> a;
+#pragma unroll
+    for (int y = 0; y < 8; ++y) {
+        a.leaf[y] = d.in[y];
+        a.extra[y] = d.extra[y];
+    }
+    a.flags = nullptr;
+    a.seq = 0;
+    a.p2 = (int)d.np;
+    a.vec_out = 1;
+    T *out = (T *)d.out;
+    const size_t n = d.count;
+    if (d.vec) {
+        constexpr int V = Pack<T>::N;
+        const size_t lanes = (n + V - 1) / V;
+        switch (d.np) {
+#define SOS_RESIDENT_FOLD(P2)                                                          \
+    case P2:                                                                           \
+        for (size_t l = threadIdx.x; l < lanes; l += kThreads)                         \
+            small_fold_lane<T, OP, P2, true, SmallFoldArgsT<8>>(out, a, n, l);         \
+        break;
+            SOS_RESIDENT_FOLD(1)
+            SOS_RESIDENT_FOLD(2)
+            SOS_RESIDENT_FOLD(4)
+            SOS_RESIDENT_FOLD(8)
+#undef SOS_RESIDENT_FOLD
+        }
+    } else {
+        for (size_t l = threadIdx.x; l < n; l += kThreads)
+            small_fold_lane<T, OP, 0, false, SmallFoldArgsT<8>>(out, a, n, l);
+    }
+}
+
+template <class T, class OP>
+__device__ __forceinline__ void resident_linear(const SosxResidentDesc &d)
+{
+    T *out = (T *)d.out;
+    const size_t n = d.count;
+    const int np = (int)d.np;
+    size_t done = 0;
+    if (d.vec) {
+        constexpr int V = Pack<T>::N;
+        const size_t nv = n / V;
+        for (size_t l = threadIdx.x; l < nv; l += kThreads) {
+            u32x4 x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (k < np) x[k] = reinterpret_cast<const u32x4 *>(d.in[k])[l];
+            u32x4 acc = x[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k)
+                if (k < np) acc = apply<T, OP>(acc, x[k]);
+            reinterpret_cast<u32x4 *>(out)[l] = acc;
+        }
+        done = nv * V;
+    }
+    for (size_t i = done + threadIdx.x; i < n; i += kThreads) {
+        T acc = ((const T *)d.in[0])[i];
+        for (int k = 1; k < np; ++k) acc = OP::f(acc, ((const T *)d.in[k])[i]);
+        out[i] = acc;
+    }
+}
+
+template <class T, class OP>
+__global__ __launch_bounds__(kThreads) void k_resident(SosxResidentCtl *c, long long idle_ticks)
+{
+    __shared__ SosxResidentDesc sd;
+    __shared__ int cmd;
+    __shared__ uint64_t cur;
+    uint64_t last = 0;
+    if (threadIdx.x == 0) last = __hip_atomic_load(&c->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    while (true) {
+        if (threadIdx.x == 0) {
+            int k = 0;  // 0: leave, 1: a request
+            const long long t0 = wall_clock64();
+            while (true) {
+                const uint64_t r = __hip_atomic_load(&c->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (r > last) {
+                    const uint64_t *src = reinterpret_cast<const uint64_t *>(&c->d);
+                    uint64_t *dst = reinterpret_cast<uint64_t *>(&sd);
+                    for (unsigned w = 0; w < sizeof(SosxResidentDesc) / 8; ++w)
+                        dst[w] = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    last = r;
+                    k = 1;
+                    break;
+                }
+                if (__hip_atomic_load(&c->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+                if (wall_clock64() - t0 > idle_ticks) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            cmd = k;
+            cur = last;
+        }
+        __syncthreads();
+        if (cmd == 0) break;
+        // every lane's loads of this request after thread 0's acquire: drop what the
+        // CU's caches hold from an earlier request at the same addresses
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (sd.kind == SOSX_RESIDENT_FOLD) resident_fold<T, OP>(sd);
+        else resident_linear<T, OP>(sd);
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(&c->done, cur, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(&c->exited, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace sos
 
 using namespace sos;
@@ -329,6 +453,15 @@ struct SmallRingFn {
 };
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+struct ResidentFn {
+    template <class T, class OP>
+    static int run(SosxResidentCtl *ctl, long long idle_ticks, hipStream_t st)
+    {
+        hipLaunchKernelGGL((k_resident<T, OP>), dim3(1), dim3(kThreads), 0, st, ctl, idle_ticks);
+        return hip_ok(hipGetLastError());
+    }
+};
 
 }  // namespace
 
@@ -455,6 +588,13 @@ int sosx_small_linear(int op, int dtype, void *out, const void *const *ins, int 
     *nblocks = (int)tiles;
     return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles,
                                  as_stream(stream));
+}
+
+// The resident executor of (op, dtype) over `ctl` (resident.h), one workgroup on `stream`.
+int sosx_resident_launch(int op, int dtype, SosxResidentCtl *ctl, long long idle_ticks, void *stream)
+{
+    if (!ctl || idle_ticks <= 0) return SOSX_ERR_ARG;
+    return dispatch<ResidentFn>(op, dtype, ctl, idle_ticks, as_stream(stream));
 }
 
 // Copy `bytes` from src (device) to dst (a node-shared slot, device view) in one

@@ -53,9 +53,11 @@
 #include <time.h>
 
 #include <atomic>
+#include <map>
 #include <vector>
 
 #include "plan.h"
+#include "resident.h"
 #include "runtime.h"
 #include "sosx.h"
 
@@ -213,6 +215,116 @@ struct SmallTrace {
 };
 SmallTrace g_strace;
 
+// ---------------------------------------------------------------------------------
+// The resident executor (resident.h; opt-in SHMEMX_SMALL_RESIDENT=1): one kernel per
+// (op, type) in use, each on a stream of its own, serving requests from pinned words.
+// ---------------------------------------------------------------------------------
+struct Resident {
+    SosxResidentCtl *ctl = nullptr;  // pinned, coherent (the same address on the device)
+    hipStream_t stream = nullptr;
+    bool running = false;
+    uint64_t seq = 0;
+};
+struct ResidentSet {
+    int on = -1;  // -1: SHMEMX_SMALL_RESIDENT not read yet
+    long long idle_ticks = 0;
+    std::map<int, Resident> by_key;  // op * 256 + dtype
+    long calls = 0, launches = 0;
+};
+ResidentSet g_res;
+
+bool resident_on()
+{
+    if (g_res.on < 0) {
+        const char *e = getenv("SHMEMX_SMALL_RESIDENT");
+        g_res.on = e && *e == '1' ? 1 : 0;
+        const char *ie = getenv("SHMEMX_SMALL_RESIDENT_IDLE_US");
+        const double idle_us = ie && *ie ? atof(ie) : 2000.0;
+        int khz = 0;
+        if (g_res.on && (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, st().device) != hipSuccess ||
+                         khz <= 0)) {
+            (void)hipGetLastError();
+            g_res.on = 0;
+        }
+        g_res.idle_ticks = (long long)((idle_us > 0 ? idle_us : 2000.0) * 1e-3 * (double)khz);
+        if (g_res.idle_ticks < 1) g_res.idle_ticks = 1;
+    }
+    return g_res.on == 1;
+}
+
+// The executor of (op, dt), created on first use; null if HIP refuses the resources.
+Resident *resident_get(int op, int dt)
+{
+    Resident &R = g_res.by_key[op * 256 + dt];
+    if (R.ctl) return &R;
+    if (hipHostMalloc((void **)&R.ctl, sizeof(SosxResidentCtl), hipHostMallocCoherent) != hipSuccess ||
+        hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        if (R.ctl) (void)hipHostFree(R.ctl);
+        g_res.by_key.erase(op * 256 + dt);
+        return nullptr;
+    }
+    memset((void *)R.ctl, 0, sizeof(SosxResidentCtl));
+    return &R;
+}
+
+void resident_launch(Resident &R, int op, int dt, const char *fn)
+{
+    if (R.running) hip_check(hipStreamSynchronize(R.stream), fn);  // the previous one has exited
+    __atomic_store_n(&R.ctl->exited, (uint64_t)0, __ATOMIC_RELAXED);
+    __atomic_store_n(&R.ctl->stop, (uint64_t)0, __ATOMIC_RELEASE);
+    const int rc = sosx_resident_launch(op, dt, R.ctl, g_res.idle_ticks, R.stream);
+    if (rc) raise_error("%s: resident small-path executor launch failed (status %d)", fn, rc);
+    R.running = true;
+    g_res.launches++;
+}
+
+// Run one request on the executor of (op, dt) and wait for its answer.  An executor seen
+// exited before answering (an idle exit racing the request) is relaunched: the new one
+// takes the pending request.
+void resident_call(int op, int dt, const SosxResidentDesc &d, const char *fn)
+{
+    Resident *R = resident_get(op, dt);
+    if (!R) raise_error("%s: resident small-path executor: HIP refused its stream or words", fn);
+    if (!R->running || __atomic_load_n(&R->ctl->exited, __ATOMIC_ACQUIRE)) resident_launch(*R, op, dt, fn);
+    R->ctl->d = d;
+    const uint64_t k = ++R->seq;
+    __atomic_store_n(&R->ctl->req, k, __ATOMIC_RELEASE);
+    const double t0 = now_s();
+    unsigned spins = 0;
+    while (__atomic_load_n(&R->ctl->done, __ATOMIC_ACQUIRE) < k) {
+        __builtin_ia32_pause();
+        if ((++spins & 0x3FF) != 0) continue;
+        if (__atomic_load_n(&R->ctl->exited, __ATOMIC_ACQUIRE) &&
+            __atomic_load_n(&R->ctl->done, __ATOMIC_ACQUIRE) < k)
+            resident_launch(*R, op, dt, fn);
+        if ((spins & 0xFFFFF) == 0) {
+            const hipError_t e = hipStreamQuery(R->stream);
+            if (e != hipSuccess && e != hipErrorNotReady) hip_check(e, fn);
+            if (now_s() - t0 > limit_s())
+                raise_error("%s: resident small-path executor: no answer after %.0f s", fn, limit_s());
+        }
+    }
+    g_res.calls++;
+}
+
+void resident_teardown()
+{
+    for (auto &kv : g_res.by_key) {
+        Resident &R = kv.second;
+        if (R.ctl) __atomic_store_n(&R.ctl->stop, (uint64_t)1, __ATOMIC_RELEASE);
+        if (R.stream) {
+            (void)hipStreamSynchronize(R.stream);
+            (void)hipStreamDestroy(R.stream);
+        }
+        if (R.ctl) (void)hipHostFree(R.ctl);
+    }
+    g_res.by_key.clear();
+    g_res.on = -1;
+}
+
+bool aligned16p(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
 }  // namespace
 
 size_t small_shared_bytes(int npes)
@@ -271,6 +383,7 @@ void small_path_setup(void *region, size_t bytes)
 
 void small_path_teardown()
 {
+    resident_teardown();
     if (g.registered && g.host) (void)hipHostUnregister(g.host);
     if (g.out) (void)hipHostFree(g.out);
     if (g.flags) (void)hipHostFree(g.flags);
@@ -278,6 +391,8 @@ void small_path_teardown()
 }
 
 long small_path_calls() { return g.calls; }
+long small_resident_calls() { return g_res.calls; }
+long small_resident_launches() { return g_res.launches; }
 long small_path_device_calls() { return g.dev_calls; }
 
 // Collective over the world when the job is up: every PE passes the same limit (checked
@@ -500,7 +615,53 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     void *out = direct ? target : g.out;  // null when this PE writes nothing
     if (++g.fseq == 0) g.fseq = 1;
     int rc = SOSX_OK, nblocks = 0;
-    if (bcast) {
+    // the resident executor (opt-in): recdbl_sw folds of up to 8 leaves and the linear
+    // folds (scans, broadcasts) of host operands up to SOSX_RESIDENT_MAX_BYTES
+    const bool resident = !staged && bytes <= SOSX_RESIDENT_MAX_BYTES && resident_on();
+    auto run_resident = [&](int rop, int rdt, uint32_t kind, int np, const void *const *ins,
+                            const void *const *extras, size_t cnt) {
+        SosxResidentDesc d;
+        memset(&d, 0, sizeof(d));
+        d.kind = kind;
+        d.np = (uint32_t)np;
+        d.count = cnt;
+        d.out = out;
+        bool vec = aligned16p(out);
+        for (int k = 0; k < np; ++k) {
+            d.in[k] = ins[k];
+            d.extra[k] = extras ? extras[k] : nullptr;
+            vec &= aligned16p(ins[k]) && (!d.extra[k] || aligned16p(d.extra[k]));
+        }
+        d.vec = vec ? 1u : 0u;
+        resident_call(rop, rdt, d, fn);
+    };
+    if (resident && bcast) {
+        const bool copy_root = ((alg - sosplan::PLAN_BCAST) & 1) != 0;
+        if (me != root || copy_root) run_resident(SOSX_OP_BOR, SOSX_DT_UCHAR, SOSX_RESIDENT_LINEAR, 1, &in[root],
+                                                  nullptr, bytes);
+        else out = nullptr;
+    } else if (resident && sosplan::is_scan(alg) && P <= 8) {
+        const int np = alg == sosplan::PLAN_INSCAN ? me + 1 : me;
+        if (np > 0) {
+            run_resident(op, dt, SOSX_RESIDENT_LINEAR, np, in, nullptr, count);
+        } else if (dev_dst) {
+            hip_check(hipMemsetAsync(out, 0, bytes, s.stream), fn);
+            hip_check(sync_system(s.stream), fn);
+        } else {
+            memset(out, 0, bytes);
+        }
+    } else if (resident && !bcast && !sosplan::is_scan(alg) && alg != SOSX_ALG_RING &&
+               sosplan::pow2_floor(P) <= 8) {
+        const int p2 = sosplan::pow2_floor(P), nx = P - p2;
+        const int mp = me < p2 ? me : me - p2;
+        const void *leaves[8], *extras[8];
+        for (int y = 0; y < p2; ++y) {
+            const int x = y ^ mp;
+            leaves[y] = in[x];
+            extras[y] = x < nx ? in[x + p2] : nullptr;
+        }
+        run_resident(op, dt, SOSX_RESIDENT_FOLD, p2, leaves, extras, count);
+    } else if (bcast) {
         // 3. one launch: the root's bytes into this PE's target -- every non-root, and the
         //    root itself for the team forms (copy_root, src/collectives_c.c4:390-397); the
         //    active-set forms leave the root's target untouched (:342-378)
@@ -614,10 +775,23 @@ bool small_local_combine(int op, int dt, void *inout, const void *in, size_t cou
     if (stage_in) memcpy(L.stage + kLocalCombineBytes, in, bytes);
     if (++L.seq == 0) L.seq = 1;
     const void *ins[2] = {io, ii};
-    int nblocks = 0;
-    const int rc = sosx_small_linear(op, dt, io, ins, 2, count, L.flags, L.seq, &nblocks, s.stream);
-    if (rc) raise_error("shmemx_reduce_local: small combine failed (status %d)", rc);
-    wait_flags(L.flags, nblocks, L.seq, "shmemx_reduce_local");
+    if (bytes <= SOSX_RESIDENT_MAX_BYTES && resident_on()) {  // the resident executor (opt-in)
+        SosxResidentDesc d;
+        memset(&d, 0, sizeof(d));
+        d.kind = SOSX_RESIDENT_LINEAR;
+        d.np = 2;
+        d.count = count;
+        d.out = io;
+        d.in[0] = io;
+        d.in[1] = ii;
+        d.vec = aligned16p(io) && aligned16p(ii) ? 1u : 0u;
+        resident_call(op, dt, d, "shmemx_reduce_local");
+    } else {
+        int nblocks = 0;
+        const int rc = sosx_small_linear(op, dt, io, ins, 2, count, L.flags, L.seq, &nblocks, s.stream);
+        if (rc) raise_error("shmemx_reduce_local: small combine failed (status %d)", rc);
+        wait_flags(L.flags, nblocks, L.seq, "shmemx_reduce_local");
+    }
     if (stage_io) memcpy(inout, L.stage, bytes);
     return true;
 }
@@ -633,6 +807,8 @@ void small_local_release()
 }  // namespace sosrt
 
 extern "C" long sosx_small_path_calls(void) { return sosrt::small_path_calls(); }
+extern "C" long sosx_small_resident_calls(void) { return sosrt::small_resident_calls(); }
+extern "C" long sosx_small_resident_launches(void) { return sosrt::small_resident_launches(); }
 extern "C" long sosx_small_path_device_calls(void) { return sosrt::small_path_device_calls(); }
 extern "C" size_t sosx_set_small_device_bytes(size_t team_bytes)
 {

@@ -172,6 +172,28 @@ def test_small_path_stress(np_):
     assert all(int(c) > 0 and int(d) > 0 for _, c, d in ok), ok
 
 
+@pytest.mark.parametrize("np_,idle", [(2, None), (4, None), (5, "50")])
+def test_small_path_resident(np_, idle):
+    """SHMEMX_SMALL_RESIDENT=1: the small path's recdbl_sw folds, scans and broadcasts of
+    host operands up to 16 KiB on the resident executor (sos_amd/csrc/resident.h), the
+    stress mix and the public scans/broadcasts, each result bit for bit the CPU oracle's.
+    A 50 us idle limit makes the executor exit between calls: relaunches then serve the
+    requests an idle exit raced (launches > 1 on some PE)."""
+    env = {"SHMEMX_SMALL_RESIDENT": "1"}
+    if idle:
+        env["SHMEMX_SMALL_RESIDENT_IDLE_US"] = idle
+    for script, pat in (("small_stress_pe.py", r"PE (\d+)/\d+: \d+ checks OK \(small-path calls"),
+                        ("coll_check_pe.py", r"PE (\d+)/\d+: \d+ checks OK \(p2p signal")):
+        r = oshrun(np_, [sys.executable, os.path.join(ROOT, "tests", script)], timeout=600, extra_env=env)
+        ok = re.findall(pat, r.stdout)
+        assert r.returncode == 0 and sorted(int(p) for p in ok) == list(range(np_)), \
+            script + r.stdout[-2000:] + r.stderr[-3000:]
+        res = re.findall(r"PE (\d+)/\d+: resident calls (\d+) launches (\d+)", r.stdout)
+        assert len(res) == np_ and all(int(c) > 0 for _, c, _ in res), (script, res)
+        if idle and script == "small_stress_pe.py":
+            assert max(int(n) for _, _, n in res) > 1, res
+
+
 @pytest.mark.parametrize("np_,signal,small_dev", [(2, "host", True), (3, "host", True),
                                                    (4, "host", False), (8, "host", True),
                                                    (3, "stream", True), (8, "stream", False)])

@@ -613,7 +613,42 @@ bool congruent16(const void *const *ps, int k, uintptr_t o)
 
 }  // namespace
 
+// Ping-pong probe of a resident ("service") kernel: one lane polls a request word in
+// pinned host memory and answers in another; the host measures the round trip.  Exits on
+// `stop`, or after `idle_ticks` of the device wall clock without a request (every wave
+// reaches the exit), storing `exited` last.
+struct PingCtl {
+    uint64_t req, done, stop, exited;
+};
+
+__global__ __launch_bounds__(64) void k_ping_service(PingCtl *c, long long idle_ticks, int nap)
+{
+    if (threadIdx.x != 0) return;
+    uint64_t last = 0;
+    long long t_idle = wall_clock64();
+    while (true) {
+        const uint64_t r = __hip_atomic_load(&c->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (r != last) {
+            last = r;
+            __hip_atomic_store(&c->done, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            t_idle = wall_clock64();
+            continue;
+        }
+        if (__hip_atomic_load(&c->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        if (wall_clock64() - t_idle > idle_ticks) break;
+        if (nap) __builtin_amdgcn_s_sleep(1);
+    }
+    __hip_atomic_store(&c->exited, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 extern "C" {
+
+int sosxv_ping_launch(void *ctl, long long idle_ticks, int nap, void *stream)
+{
+    hipLaunchKernelGGL(k_ping_service, dim3(1), dim3(64), 0, as_stream(stream), (PingCtl *)ctl, idle_ticks, nap);
+    return hip_ok(hipGetLastError());
+}
+
 
 int sosxv_num_combine(void) { return kNumCombine; }
 const char *sosxv_combine_name(int v) { return v >= 0 && v < kNumCombine ? kCombineNames[v] : ""; }
