@@ -5,9 +5,12 @@
 // (profiles/r5_sync_cost.json); a request/answer round trip through a kernel that stays
 // resident and polls pinned host memory costs 1.7 us (profiles/r5_resident.txt).  With
 // SHMEMX_SMALL_RESIDENT=1 the small shared-memory path's recdbl_sw folds and linear folds
-// (scans, broadcasts) of host operands run on such a kernel: one per (type, op) used,
-// one workgroup, launched on the first request and exiting on its own after
-// SHMEMX_SMALL_RESIDENT_IDLE_US of idleness (default 2000) or at shmem_finalize.
+// (scans, broadcasts) of host operands, and shmemx_reduce_local's small combines, run on
+// such a kernel: one per (type, op) used, one workgroup, launched on the first request
+// and exiting on its own after SHMEMX_SMALL_RESIDENT_IDLE_US of idleness (default 2000)
+// or at shmem_finalize.  Measured gain at P = 2 / 4 on one GPU: 0.5-2 us of a 10-13 us
+// call -- the request's host-link round trips (descriptor, slots, result + fence) cost
+// what the launch saved -- so it stays opt-in (profiles/r5_resident.txt).
 //
 // Protocol (every word in pinned, coherent host memory):
 //   host  : write the descriptor d, then req = k (release);
@@ -21,7 +24,7 @@
 
 #define SOSX_RESIDENT_FOLD 0    /* recdbl_sw tree over np leaves (+ extras): k_small_fold's value */
 #define SOSX_RESIDENT_LINEAR 1  /* in[0] OP in[1] ... OP in[np-1]: k_small_ring's single chunk */
-#define SOSX_RESIDENT_MAX_BYTES (16 * 1024)
+#define SOSX_RESIDENT_MAX_BYTES 4096   /* one pass of the workgroup (256 lanes x 16 B); larger calls launch */
 
 struct SosxResidentDesc {
     uint32_t kind;

@@ -347,10 +347,6 @@ __global__ __launch_bounds__(kThreads) void k_resident(SosxResidentCtl *c, long 
             while (true) {
                 const uint64_t r = __hip_atomic_load(&c->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (r > last) {
-                    const uint64_t *src = reinterpret_cast<const uint64_t *>(&c->d);
-                    uint64_t *dst = reinterpret_cast<uint64_t *>(&sd);
-                    for (unsigned w = 0; w < sizeof(SosxResidentDesc) / 8; ++w)
-                        dst[w] = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     last = r;
                     k = 1;
                     break;
@@ -367,6 +363,12 @@ __global__ __launch_bounds__(kThreads) void k_resident(SosxResidentCtl *c, long 
         // every lane's loads of this request after thread 0's acquire: drop what the
         // CU's caches hold from an earlier request at the same addresses
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        // the descriptor, one word per lane (one host-link round trip, not one per word)
+        constexpr unsigned kDescWords = sizeof(SosxResidentDesc) / 8;
+        if (threadIdx.x < kDescWords)
+            reinterpret_cast<uint64_t *>(&sd)[threadIdx.x] = __hip_atomic_load(
+                reinterpret_cast<const uint64_t *>(&c->d) + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
         if (sd.kind == SOSX_RESIDENT_FOLD) resident_fold<T, OP>(sd);
         else resident_linear<T, OP>(sd);
         __threadfence_system();

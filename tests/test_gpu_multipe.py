@@ -175,7 +175,7 @@ def test_small_path_stress(np_):
 @pytest.mark.parametrize("np_,idle", [(2, None), (4, None), (5, "50")])
 def test_small_path_resident(np_, idle):
     """SHMEMX_SMALL_RESIDENT=1: the small path's recdbl_sw folds, scans and broadcasts of
-    host operands up to 16 KiB on the resident executor (sos_amd/csrc/resident.h), the
+    host operands up to 4 KiB on the resident executor (sos_amd/csrc/resident.h), the
     stress mix and the public scans/broadcasts, each result bit for bit the CPU oracle's.
     A 50 us idle limit makes the executor exit between calls: relaunches then serve the
     requests an idle exit raced (launches > 1 on some PE)."""

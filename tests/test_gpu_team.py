@@ -242,7 +242,7 @@ def test_reduce_local_small(torch_cuda, shmem1, oracle, dt, op):
 
 def test_reduce_local_small_resident():
     """The same calls with SHMEMX_SMALL_RESIDENT=1 (a fresh process): combines of at most
-    16 KiB on the resident executor, the rest on launches, every result the oracle's; then
+    4 KiB on the resident executor, the rest on launches, every result the oracle's; then
     with a 50 us idle limit, so the executor exits between calls and is relaunched."""
     here = os.path.abspath(__file__)
     for idle in ("2000", "50"):
