@@ -5,8 +5,8 @@
 // (profiles/r5_sync_cost.json); a request/answer round trip through a kernel that stays
 // resident and polls pinned host memory costs 1.7 us (profiles/r5_resident.txt).  With
 // SHMEMX_SMALL_RESIDENT=1 the small shared-memory path's recdbl_sw folds and linear folds
-// (scans, broadcasts) of host operands, and shmemx_reduce_local's small combines, run on
-// such a kernel: one per (type, op) used, one workgroup, launched on the first request
+// (scans, broadcasts), the staging of device operands into their slots, and
+// shmemx_reduce_local's small combines run on such a kernel: one per (type, op) used, one workgroup, launched on the first request
 // and exiting on its own after SHMEMX_SMALL_RESIDENT_IDLE_US of idleness (default 2000)
 // or at shmem_finalize.  Measured gain at P = 2 / 4 on one GPU: 0.5-2 us of a 10-13 us
 // call -- the request's host-link round trips (descriptor, slots, result + fence) cost
@@ -24,6 +24,9 @@
 
 #define SOSX_RESIDENT_FOLD 0    /* recdbl_sw tree over np leaves (+ extras): k_small_fold's value */
 #define SOSX_RESIDENT_LINEAR 1  /* in[0] OP in[1] ... OP in[np-1]: k_small_ring's single chunk */
+#define SOSX_RESIDENT_STAGE 2   /* count bytes in[0] -> out (a device operand into its slot), a
+                                   system-scope fence, then *word[k] = val[k], k < np (the posts):
+                                   k_small_stage's work */
 #define SOSX_RESIDENT_MAX_BYTES 4096   /* one pass of the workgroup (256 lanes x 16 B); larger calls launch */
 
 struct SosxResidentDesc {
@@ -33,6 +36,8 @@ struct SosxResidentDesc {
     void *out;
     const void *in[8];
     const void *extra[8];        /* FOLD: null where the leaf has no extra PE */
+    uint64_t *word[8];           /* STAGE: the post words (device views) */
+    uint64_t val[8];             /* STAGE: their values */
     uint32_t vec;                /* every operand 16-B aligned: 16-B vectors per lane */
     uint32_t pad;
 };

@@ -332,6 +332,26 @@ __device__ __forceinline__ void resident_linear(const SosxResidentDesc &d)
     }
 }
 
+// k_small_stage's work in the resident workgroup: the operand's bytes into the slot, a
+// system-scope fence by every lane, then the posts (one lane each, after the barrier).
+__device__ __forceinline__ void resident_stage(const SosxResidentDesc &d)
+{
+    const uint8_t *s = (const uint8_t *)d.in[0];
+    uint8_t *o = (uint8_t *)d.out;
+    uint64_t done = 0;
+    if (d.vec) {
+        const uint64_t nv = d.count / 16;
+        for (uint64_t i = threadIdx.x; i < nv; i += kThreads)
+            reinterpret_cast<u32x4 *>(o)[i] = reinterpret_cast<const u32x4 *>(s)[i];
+        done = nv * 16;
+    }
+    for (uint64_t i = done + threadIdx.x; i < d.count; i += kThreads) o[i] = s[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x < d.np)
+        __hip_atomic_store(d.word[threadIdx.x], d.val[threadIdx.x], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <class T, class OP>
 __global__ __launch_bounds__(kThreads) void k_resident(SosxResidentCtl *c, long long idle_ticks)
 {
@@ -370,6 +390,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(SosxResidentCtl *c, long 
                 reinterpret_cast<const uint64_t *>(&c->d) + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __syncthreads();
         if (sd.kind == SOSX_RESIDENT_FOLD) resident_fold<T, OP>(sd);
+        else if (sd.kind == SOSX_RESIDENT_STAGE) resident_stage(sd);
         else resident_linear<T, OP>(sd);
         __threadfence_system();
         __syncthreads();

@@ -587,7 +587,27 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         }
         g.slot_users[sl].push_back({r, k});
     }
-    if (staged) {
+    // the resident executor (opt-in) takes requests up to SOSX_RESIDENT_MAX_BYTES: a device
+    // operand's staging + posts then run there too (and the fold after it, below)
+    const bool res_ok = bytes <= SOSX_RESIDENT_MAX_BYTES && resident_on();
+    const bool staged_res = staged && res_ok && nw <= 8;
+    if (staged_res) {
+        std::atomic_thread_fence(std::memory_order_seq_cst);  // the slot ids before the request
+        SosxResidentDesc d;
+        memset(&d, 0, sizeof(d));
+        d.kind = SOSX_RESIDENT_STAGE;
+        d.np = (uint32_t)nw;
+        d.count = bytes;
+        d.out = g.dev + slot_off(mw, sl);
+        d.in[0] = source;
+        for (int k = 0; k < nw; ++k) {
+            d.word[k] = words[k];
+            d.val[k] = vals[k];
+        }
+        d.vec = aligned16p(source) && aligned16p(d.out) ? 1u : 0u;
+        if (bcast) resident_call(SOSX_OP_BOR, SOSX_DT_UCHAR, d, fn);
+        else resident_call(op, dt, d, fn);
+    } else if (staged) {
         std::atomic_thread_fence(std::memory_order_seq_cst);  // the slot ids before the launch
         const int rc = sosx_small_stage(g.dev + slot_off(mw, sl), source, bytes, words, vals, nw, s.stream);
         if (rc) raise_error("%s: small-path copy of a device operand failed (status %d)", fn, rc);
@@ -616,8 +636,8 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     if (++g.fseq == 0) g.fseq = 1;
     int rc = SOSX_OK, nblocks = 0;
     // the resident executor (opt-in): recdbl_sw folds of up to 8 leaves and the linear
-    // folds (scans, broadcasts) of host operands up to SOSX_RESIDENT_MAX_BYTES
-    const bool resident = !staged && bytes <= SOSX_RESIDENT_MAX_BYTES && resident_on();
+    // folds (scans, broadcasts), unless a launched staging copy precedes them on the stream
+    const bool resident = res_ok && (!staged || staged_res);
     auto run_resident = [&](int rop, int rdt, uint32_t kind, int np, const void *const *ins,
                             const void *const *extras, size_t cnt) {
         SosxResidentDesc d;
@@ -704,7 +724,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     if (rc) raise_error("%s: small-path reduction failed (status %d)", fn, rc);
     // no fold launch followed the copy kernel (an active-set broadcast's root, exscan's
     // PE 0 with a host target): the call must not return while it still reads `source`
-    if (staged && nblocks == 0) hip_check(sync_system(s.stream), fn);
+    if (staged && !staged_res && nblocks == 0) hip_check(sync_system(s.stream), fn);
     phase(3);
     // 4. completion from the workgroups' flags (no stream synchronisation); then the
     //    peers' slots are read: acknowledge; my result out
