@@ -59,6 +59,36 @@ def main():
             w[2] = 1  # stop
             HIP.hipStreamSynchronize(sp)
             assert w[3] == 1
+    # request word in fine-grained device memory (the host writes it over the link, the
+    # kernel polls it locally), answer in pinned host memory (the host polls it locally)
+    v.sosxv_ping_split_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]
+    dreq = ctypes.c_void_p()
+    rc = HIP.hipExtMallocWithFlags(ctypes.byref(dreq), ctypes.c_size_t(4096), ctypes.c_uint(0x1))  # fine-grained
+    name = "split: request in fine-grained device memory, answer in host memory"
+    if rc == 0:
+        req = (ctypes.c_uint64 * 1).from_address(dreq.value)
+        res[name] = []
+        try:
+            for _ in range(a.rounds):
+                req[0] = 0
+                w[0] = w[1] = w[2] = w[3] = 0
+                assert v.sosxv_ping_split_launch(dreq, ctl, ctypes.c_longlong(200_000_000), sp) == 0
+                req[0] = 1
+                t0 = time.perf_counter()
+                while w[0] != 1:
+                    if time.perf_counter() - t0 > 5:
+                        raise SystemExit("split resident kernel did not answer")
+                t0 = time.perf_counter()
+                for k in range(2, a.iters + 2):
+                    req[0] = k
+                    while w[0] != k:
+                        pass
+                res[name].append((time.perf_counter() - t0) / a.iters * 1e6)
+                req[0] = 0xFFFFFFFFFFFFFFFF
+                HIP.hipStreamSynchronize(sp)
+        except Exception as e:  # host access to the allocation refused
+            res[name] = [float("nan")]
+            print(f"split leg failed: {e}", file=sys.stderr)
     out = {k: {"median_us": round(statistics.median(x), 3), "rounds_us": [round(t, 3) for t in x]}
            for k, x in res.items()}
     print(json.dumps({"what": "host us per request/answer round trip through a resident kernel "

@@ -641,7 +641,35 @@ __global__ __launch_bounds__(64) void k_ping_service(PingCtl *c, long long idle_
     __hip_atomic_store(&c->exited, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The same with the request word where the kernel polls it (device memory the host
+// writes over the link) and the answer where the host polls it (pinned host memory).
+__global__ __launch_bounds__(64) void k_ping_split(uint64_t *req, uint64_t *ans, long long idle_ticks)
+{
+    if (threadIdx.x != 0) return;
+    uint64_t last = 0;
+    long long t_idle = wall_clock64();
+    while (true) {
+        const uint64_t r = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (r == ~0ull) break;  // stop
+        if (r != last) {
+            last = r;
+            __hip_atomic_store(ans, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            t_idle = wall_clock64();
+            continue;
+        }
+        if (wall_clock64() - t_idle > idle_ticks) break;
+    }
+    __hip_atomic_store(ans + 1, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 extern "C" {
+
+int sosxv_ping_split_launch(void *req, void *ans, long long idle_ticks, void *stream)
+{
+    hipLaunchKernelGGL(k_ping_split, dim3(1), dim3(64), 0, as_stream(stream), (uint64_t *)req, (uint64_t *)ans,
+                       idle_ticks);
+    return hip_ok(hipGetLastError());
+}
 
 int sosxv_ping_launch(void *ctl, long long idle_ticks, int nap, void *stream)
 {
