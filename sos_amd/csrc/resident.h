@@ -24,22 +24,41 @@
 
 #define SOSX_RESIDENT_FOLD 0    /* recdbl_sw tree over np leaves (+ extras): k_small_fold's value */
 #define SOSX_RESIDENT_LINEAR 1  /* in[0] OP in[1] ... OP in[np-1]: k_small_ring's single chunk */
-#define SOSX_RESIDENT_STAGE 2   /* count bytes in[0] -> out (a device operand into its slot), a
-                                   system-scope fence, then *word[k] = val[k], k < np (the posts):
-                                   k_small_stage's work */
+#define SOSX_RESIDENT_STAGE 2   /* stage_bytes stage_src -> stage_dst (a device operand into its slot),
+                                   a system-scope fence, then *post_word[k] = post_val[k], k < nposts
+                                   (the posts): k_small_stage's work */
+#define SOSX_RESIDENT_STAGE_FOLD 3  /* STAGE, then for each team member i < npeers wait until
+                                   *wait_word[i] >= wait_val[i] (bounded by `limit` ticks), take its
+                                   slot slot[i][*ring_word[i]] (wait_word null: slot[i][0], the PE's
+                                   own), and FOLD over leaves leaf_idx[y] (+ extras extra_idx[y] >= 0)
+                                   of those: the device-operand recdbl_sw call in one request */
 #define SOSX_RESIDENT_MAX_BYTES 4096   /* one pass of the workgroup (256 lanes x 16 B); larger calls launch */
 
 struct SosxResidentDesc {
     uint32_t kind;
     uint32_t np;                 /* leaves (FOLD: 1, 2, 4, 8) or inputs (LINEAR: 1..8) */
-    uint64_t count;              /* elements, count * size <= SOSX_RESIDENT_MAX_BYTES */
+    uint64_t count;              /* fold elements, count * size <= SOSX_RESIDENT_MAX_BYTES */
     void *out;
     const void *in[8];
     const void *extra[8];        /* FOLD: null where the leaf has no extra PE */
-    uint64_t *word[8];           /* STAGE: the post words (device views) */
-    uint64_t val[8];             /* STAGE: their values */
-    uint32_t vec;                /* every operand 16-B aligned: 16-B vectors per lane */
-    uint32_t pad;
+    uint32_t vec;                /* every fold operand 16-B aligned: 16-B vectors per lane */
+    uint32_t nposts;
+    /* STAGE / STAGE_FOLD */
+    const void *stage_src;
+    void *stage_dst;
+    uint64_t stage_bytes;
+    uint32_t stage_vec;
+    uint32_t npeers;
+    uint64_t *post_word[8];      /* device views */
+    uint64_t post_val[8];
+    /* STAGE_FOLD */
+    const uint64_t *wait_word[8];
+    uint64_t wait_val[8];
+    const uint32_t *ring_word[8];
+    const void *slot[8][2];
+    int8_t leaf_idx[8];
+    int8_t extra_idx[8];         /* -1: none */
+    long long limit;
 };
 
 struct SosxResidentCtl {
@@ -47,7 +66,8 @@ struct SosxResidentCtl {
     uint64_t done;
     uint64_t stop;
     uint64_t exited;
-    uint64_t pad[4];
+    uint64_t err;                /* a STAGE_FOLD wait timed out (the host turns it into an error) */
+    uint64_t pad[3];
     struct SosxResidentDesc d;
 };
 

@@ -336,20 +336,68 @@ __device__ __forceinline__ void resident_linear(const SosxResidentDesc &d)
 // system-scope fence by every lane, then the posts (one lane each, after the barrier).
 __device__ __forceinline__ void resident_stage(const SosxResidentDesc &d)
 {
-    const uint8_t *s = (const uint8_t *)d.in[0];
-    uint8_t *o = (uint8_t *)d.out;
+    const uint8_t *s = (const uint8_t *)d.stage_src;
+    uint8_t *o = (uint8_t *)d.stage_dst;
     uint64_t done = 0;
-    if (d.vec) {
-        const uint64_t nv = d.count / 16;
+    if (d.stage_vec) {
+        const uint64_t nv = d.stage_bytes / 16;
         for (uint64_t i = threadIdx.x; i < nv; i += kThreads)
             reinterpret_cast<u32x4 *>(o)[i] = reinterpret_cast<const u32x4 *>(s)[i];
         done = nv * 16;
     }
-    for (uint64_t i = done + threadIdx.x; i < d.count; i += kThreads) o[i] = s[i];
+    for (uint64_t i = done + threadIdx.x; i < d.stage_bytes; i += kThreads) o[i] = s[i];
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x < d.np)
-        __hip_atomic_store(d.word[threadIdx.x], d.val[threadIdx.x], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x < d.nposts)
+        __hip_atomic_store(d.post_word[threadIdx.x], d.post_val[threadIdx.x], __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// STAGE_FOLD after the staging: lane i < npeers waits for team member i's post (bounded:
+// on expiry it flags *err, and the fold is skipped), reads the slot id it posted in and
+// resolves its operand; then the leaves of the fold are taken from those operands.
+// Returns false when a wait expired.
+__device__ __forceinline__ bool resident_gather_slots(SosxResidentDesc &d, SosxResidentCtl *c)
+{
+    __shared__ const void *opnd[8];
+    __shared__ int expired;
+    if (threadIdx.x == 0) expired = 0;
+    __syncthreads();
+    const unsigned i = threadIdx.x;
+    if (i < d.npeers) {
+        if (!d.wait_word[i]) {
+            opnd[i] = d.slot[i][0];
+        } else {
+            const long long t0 = wall_clock64();
+            bool ok = true;
+            while (__hip_atomic_load(d.wait_word[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < d.wait_val[i]) {
+                if (wall_clock64() - t0 > d.limit) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (ok) {
+                const uint32_t r = __hip_atomic_load(d.ring_word[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                opnd[i] = d.slot[i][r & 1];
+            } else {
+                expired = 1;
+                __hip_atomic_store(&c->err, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+    __syncthreads();
+    if (expired) return false;
+    // the peers' slot bytes after their posts: every lane acquires before its loads
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (threadIdx.x == 0) {
+        for (unsigned y = 0; y < d.np; ++y) {
+            d.in[y] = opnd[d.leaf_idx[y]];
+            d.extra[y] = d.extra_idx[y] >= 0 ? opnd[d.extra_idx[y]] : nullptr;
+        }
+    }
+    __syncthreads();
+    return true;
 }
 
 template <class T, class OP>
@@ -389,9 +437,16 @@ __global__ __launch_bounds__(kThreads) void k_resident(SosxResidentCtl *c, long 
             reinterpret_cast<uint64_t *>(&sd)[threadIdx.x] = __hip_atomic_load(
                 reinterpret_cast<const uint64_t *>(&c->d) + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __syncthreads();
-        if (sd.kind == SOSX_RESIDENT_FOLD) resident_fold<T, OP>(sd);
-        else if (sd.kind == SOSX_RESIDENT_STAGE) resident_stage(sd);
-        else resident_linear<T, OP>(sd);
+        if (sd.kind == SOSX_RESIDENT_FOLD) {
+            resident_fold<T, OP>(sd);
+        } else if (sd.kind == SOSX_RESIDENT_STAGE) {
+            resident_stage(sd);
+        } else if (sd.kind == SOSX_RESIDENT_STAGE_FOLD) {
+            resident_stage(sd);
+            if (resident_gather_slots(sd, c)) resident_fold<T, OP>(sd);
+        } else {
+            resident_linear<T, OP>(sd);
+        }
         __threadfence_system();
         __syncthreads();
         if (threadIdx.x == 0) __hip_atomic_store(&c->done, cur, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -53,6 +53,7 @@
 #include <time.h>
 
 #include <atomic>
+#include <functional>
 #include <map>
 #include <vector>
 
@@ -230,6 +231,7 @@ struct ResidentSet {
     long long idle_ticks = 0;
     std::map<int, Resident> by_key;  // op * 256 + dtype
     long calls = 0, launches = 0;
+    int khz = 0;                     // device wall clock (kHz)
 };
 ResidentSet g_res;
 
@@ -246,6 +248,7 @@ bool resident_on()
             (void)hipGetLastError();
             g_res.on = 0;
         }
+        g_res.khz = khz;
         g_res.idle_ticks = (long long)((idle_us > 0 ? idle_us : 2000.0) * 1e-3 * (double)khz);
         if (g_res.idle_ticks < 1) g_res.idle_ticks = 1;
     }
@@ -282,7 +285,8 @@ void resident_launch(Resident &R, int op, int dt, const char *fn)
 // Run one request on the executor of (op, dt) and wait for its answer.  An executor seen
 // exited before answering (an idle exit racing the request) is relaunched: the new one
 // takes the pending request.
-void resident_call(int op, int dt, const SosxResidentDesc &d, const char *fn)
+void resident_call(int op, int dt, const SosxResidentDesc &d, const char *fn,
+                   const std::function<void()> &poll = {})
 {
     Resident *R = resident_get(op, dt);
     if (!R) raise_error("%s: resident small-path executor: HIP refused its stream or words", fn);
@@ -294,7 +298,8 @@ void resident_call(int op, int dt, const SosxResidentDesc &d, const char *fn)
     unsigned spins = 0;
     while (__atomic_load_n(&R->ctl->done, __ATOMIC_ACQUIRE) < k) {
         __builtin_ia32_pause();
-        if ((++spins & 0x3FF) != 0) continue;
+        if ((++spins & 0xFF) == 0 && poll) poll();
+        if ((spins & 0x3FF) != 0) continue;
         if (__atomic_load_n(&R->ctl->exited, __ATOMIC_ACQUIRE) &&
             __atomic_load_n(&R->ctl->done, __ATOMIC_ACQUIRE) < k)
             resident_launch(*R, op, dt, fn);
@@ -306,6 +311,11 @@ void resident_call(int op, int dt, const SosxResidentDesc &d, const char *fn)
         }
     }
     g_res.calls++;
+    if (__atomic_load_n(&R->ctl->err, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(&R->ctl->err, (uint64_t)0, __ATOMIC_RELAXED);
+        raise_error("%s: small shared-memory path: timed out after %.0f s waiting for a peer's operand "
+                    "(resident executor)", fn, limit_s());
+    }
 }
 
 void resident_teardown()
@@ -478,27 +488,37 @@ const char *route_text(uint64_t tag)
 // peer that took the executor for this call (its route word for the call says so, or it
 // has moved past the call without posting) ends the job at once with both PEs' operands
 // named, instead of after SHMEMX_P2P_TIMEOUT.
+// While q's kp-th post is missing: q's route word says whether it took the other path
+// for this call (ends the job at once, both PEs' operands named).  `past`: when q was
+// first seen past the call with the post missing.
+void route_check(int q, uint64_t kp, uint64_t mine, const char *fn, double &past)
+{
+    const int mw = st().my_pe;
+    const std::atomic<uint64_t> &w = ctl(q)->posted[mw].v;
+    const uint64_t v = ctl(q)->route[mw].v.load(std::memory_order_acquire);
+    const uint64_t ik = v >> 8, rk = g.route_k[q];
+    if (ik == rk && !(v & kRouteSmall)) route_mismatch(fn, mine, q, v & 0xFF, true);
+    if (ik > rk && w.load(std::memory_order_acquire) < kp) {
+        // q finished this call: on the small path its post came first (a device post
+        // is stored by the copy kernel before q's fold can finish); allow the write
+        // 10 ms to arrive before calling it a disagreement
+        if (past == 0) past = now_s();
+        else if (now_s() - past > 0.01) route_mismatch(fn, mine, q, 0, false);
+    }
+}
+
 void wait_post(int q, uint64_t kp, uint64_t mine, const char *fn)
 {
     const int mw = st().my_pe;
     const std::atomic<uint64_t> &w = ctl(q)->posted[mw].v;
     if (w.load(std::memory_order_acquire) >= kp) return;
     const double t0 = now_s();
-    double past = 0;  // when q was first seen past the call with the post missing
+    double past = 0;
     unsigned spins = 0;
     while (w.load(std::memory_order_acquire) < kp) {
         __builtin_ia32_pause();
         if ((++spins & 0xFF) != 0) continue;
-        const uint64_t v = ctl(q)->route[mw].v.load(std::memory_order_acquire);
-        const uint64_t ik = v >> 8, rk = g.route_k[q];
-        if (ik == rk && !(v & kRouteSmall)) route_mismatch(fn, mine, q, v & 0xFF, true);
-        if (ik > rk && w.load(std::memory_order_acquire) < kp) {
-            // q finished this call: on the small path its post came first (a device post
-            // is stored by the copy kernel before q's fold can finish); allow the write
-            // 10 ms to arrive before calling it a disagreement
-            if (past == 0) past = now_s();
-            else if (now_s() - past > 0.01) route_mismatch(fn, mine, q, 0, false);
-        }
+        route_check(q, kp, mine, fn, past);
         if ((spins & 0xFFFF) == 0 && now_s() - t0 > limit_s())
             raise_error("small shared-memory path: timed out after %.0f s waiting for a peer's operand",
                         limit_s());
@@ -591,22 +611,75 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     // operand's staging + posts then run there too (and the fold after it, below)
     const bool res_ok = bytes <= SOSX_RESIDENT_MAX_BYTES && resident_on();
     const bool staged_res = staged && res_ok && nw <= 8;
+    // a recdbl_sw reduction of a device operand in ONE request: staging + posts, the waits
+    // for the peers' posts on the device, the fold
+    const bool fused = staged_res && !bcast && !sosplan::is_scan(alg) && alg != SOSX_ALG_RING && P <= 8;
     if (staged_res) {
         std::atomic_thread_fence(std::memory_order_seq_cst);  // the slot ids before the request
         SosxResidentDesc d;
         memset(&d, 0, sizeof(d));
-        d.kind = SOSX_RESIDENT_STAGE;
-        d.np = (uint32_t)nw;
-        d.count = bytes;
-        d.out = g.dev + slot_off(mw, sl);
-        d.in[0] = source;
+        d.kind = fused ? SOSX_RESIDENT_STAGE_FOLD : SOSX_RESIDENT_STAGE;
+        d.stage_src = source;
+        d.stage_dst = g.dev + slot_off(mw, sl);
+        d.stage_bytes = bytes;
+        d.stage_vec = aligned16p(source) && aligned16p(d.stage_dst) ? 1u : 0u;
+        d.nposts = (uint32_t)nw;
         for (int k = 0; k < nw; ++k) {
-            d.word[k] = words[k];
-            d.val[k] = vals[k];
+            d.post_word[k] = words[k];
+            d.post_val[k] = vals[k];
         }
-        d.vec = aligned16p(source) && aligned16p(d.out) ? 1u : 0u;
-        if (bcast) resident_call(SOSX_OP_BOR, SOSX_DT_UCHAR, d, fn);
-        else resident_call(op, dt, d, fn);
+        if (!fused) {
+            if (bcast) resident_call(SOSX_OP_BOR, SOSX_DT_UCHAR, d, fn);
+            else resident_call(op, dt, d, fn);
+        } else {
+            phase(1);
+            int from[8];
+            uint64_t want[8];
+            d.npeers = (uint32_t)P;
+            for (int i = 0; i < P; ++i) {
+                from[i] = -1;
+                if (i == me) {
+                    d.slot[i][0] = g.dev + slot_off(mw, sl);
+                    continue;
+                }
+                const int q = t.world_rank(i);
+                const uint64_t k = ++g.seen_from[q];
+                SmallCtl *qc = ctl(q);
+                d.wait_word[i] = (const uint64_t *)(g.dev + ((char *)&qc->posted[mw].v - g.host));
+                d.wait_val[i] = k;
+                d.ring_word[i] = (const uint32_t *)(g.dev + ((char *)&qc->ring[mw][k % 2] - g.host));
+                d.slot[i][0] = g.dev + slot_off(q, 0);
+                d.slot[i][1] = g.dev + slot_off(q, 1);
+                from[i] = q;
+                want[i] = k;
+            }
+            const int p2 = sosplan::pow2_floor(P), nx = P - p2;
+            const int mp = me < p2 ? me : me - p2;
+            d.np = (uint32_t)p2;
+            for (int y = 0; y < p2; ++y) {
+                const int x = y ^ mp;
+                d.leaf_idx[y] = (int8_t)x;
+                d.extra_idx[y] = (int8_t)(x < nx ? x + p2 : -1);
+            }
+            const bool direct = dev_dst || s.host_heap.contains(target, bytes);
+            d.out = direct ? target : g.out;
+            d.count = count;
+            d.vec = aligned16p(d.out) ? 1u : 0u;  // the slots are 16-B aligned
+            d.limit = (long long)(limit_s() * 1e3 * (double)g_res.khz);
+            double past[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            resident_call(op, dt, d, fn, [&]() {  // a peer that took the other path ends the job
+                for (int i = 0; i < P; ++i)
+                    if (from[i] >= 0 && ctl(from[i])->posted[mw].v.load(std::memory_order_acquire) < want[i])
+                        route_check(from[i], want[i], g.route_tag, fn, past[i]);
+            });
+            phase(3);
+            for (int i = 0; i < P; ++i)
+                if (from[i] >= 0) mine->consumed[from[i]].v.store(g.seen_from[from[i]], std::memory_order_release);
+            if (!direct) memcpy(target, g.out, bytes);
+            g.calls++;
+            g.dev_calls++;
+            return;
+        }
     } else if (staged) {
         std::atomic_thread_fence(std::memory_order_seq_cst);  // the slot ids before the launch
         const int rc = sosx_small_stage(g.dev + slot_off(mw, sl), source, bytes, words, vals, nw, s.stream);
