@@ -227,14 +227,18 @@ def test_p2p_wait_is_bounded(signal):
     assert time.monotonic() - t0 < 55, "the job outlived the late PE's sleep"
 
 
-@pytest.mark.parametrize("mode", ["host", "devsmall"])
-def test_small_path_wait_is_bounded(mode):
+@pytest.mark.parametrize("mode,resident", [("host", False), ("devsmall", False), ("devsmall", True)])
+def test_small_path_wait_is_bounded(mode, resident):
     """The same late PE with 64-float operands in the host heap or the device heap: the
     call takes the small path through node shared memory, whose waits for a peer's operand
-    are bounded by SHMEMX_P2P_TIMEOUT too."""
+    are bounded by SHMEMX_P2P_TIMEOUT too -- on the resident executor (a device operand's
+    call as one request) the device-side wait is."""
     t0 = time.monotonic()
+    env = {"SHMEMX_P2P_TIMEOUT": "3"}
+    if resident:
+        env["SHMEMX_SMALL_RESIDENT"] = "1"
     r = oshrun(2, [sys.executable, os.path.join(ROOT, "tests", "p2p_timeout_pe.py"), mode],
-               timeout=150, extra_env={"SHMEMX_P2P_TIMEOUT": "3"})
+               timeout=150, extra_env=env)
     assert r.returncode != 0, r.stdout
     assert "small shared-memory path: timed out" in r.stderr, r.stderr[-2000:]
     assert "reduction returned" not in r.stdout
