@@ -38,7 +38,10 @@
 // over the host link costs as much as the exchange saves, or more.  The path takes device
 // operands while P * bytes <= SHMEMX_SMALL_DEVICE (default 128 KiB).  The GPU-side posts
 // do not shorten the critical path (a peer's fold still launches after the post arrives);
-// they save the host a completion round trip.
+// they save the host a completion round trip.  With SHMEMX_SMALL_RESIDENT=1 (resident.h)
+// calls up to 4 KiB per operand run as requests to a resident kernel instead of launches;
+// a device operand's recdbl_sw call is then ONE request: staging, posts, the waits for
+// the peers' posts (on the device, bounded) and the fold.
 //
 // Slot reuse: each PE alternates between two data slots.  A post to receiver r carries
 // a per-pair index k (posted[q][r] = k) and the slot id (ring[q][r][k % 2]); receiver r
