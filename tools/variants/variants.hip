@@ -662,7 +662,48 @@ __global__ __launch_bounds__(64) void k_ping_split(uint64_t *req, uint64_t *ans,
     __hip_atomic_store(ans + 1, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Stream ceilings (tools/stream_ceiling.py): the same tile shape as k_combine3 (one 16-B
+// vector per lane per stream, nontemporal, one tile per workgroup) with R read streams and
+// W write streams: R=1,W=0 read-only (the lanes' xor is stored only when impossible, so
+// the loads stay), R=0,W=1 write-only, R=1,W=1 copy, R=2,W=1 the combine's shape.
+template <int R, int W>
+__global__ __launch_bounds__(kThreads) void k_stream(u32x4 *out, const u32x4 *a, const u32x4 *b, size_t nvec,
+                                                     unsigned never)
+{
+    const size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= nvec) return;
+    u32x4 x = {0u, 0u, 0u, 0u};
+    if constexpr (R >= 1) x = __builtin_nontemporal_load(a + i);
+    if constexpr (R >= 2) {
+        const u32x4 y = __builtin_nontemporal_load(b + i);
+        x = x ^ y;
+    }
+    if constexpr (W >= 1) {
+        if constexpr (R == 0) x = u32x4{(unsigned)i, 1u, 2u, 3u};
+        __builtin_nontemporal_store(x, out + i);
+    } else {
+        if (x[0] == never && x[1] == never && x[2] == never && x[3] == never) out[i] = x;
+    }
+}
+
 extern "C" {
+
+// kind 0 read-only, 1 write-only, 2 copy, 3 two reads + one write; nvec 16-B vectors.
+int sosxv_stream(int kind, void *out, const void *a, const void *b, size_t nvec, void *stream)
+{
+    const unsigned blocks = (unsigned)((nvec + kThreads - 1) / kThreads);
+    const hipStream_t st = as_stream(stream);
+    u32x4 *o = (u32x4 *)out;
+    const u32x4 *x = (const u32x4 *)a, *y = (const u32x4 *)b;
+    switch (kind) {
+        case 0: hipLaunchKernelGGL((k_stream<1, 0>), dim3(blocks), dim3(kThreads), 0, st, o, x, y, nvec, 0x9E3779B9u); break;
+        case 1: hipLaunchKernelGGL((k_stream<0, 1>), dim3(blocks), dim3(kThreads), 0, st, o, x, y, nvec, 0u); break;
+        case 2: hipLaunchKernelGGL((k_stream<1, 1>), dim3(blocks), dim3(kThreads), 0, st, o, x, y, nvec, 0u); break;
+        case 3: hipLaunchKernelGGL((k_stream<2, 1>), dim3(blocks), dim3(kThreads), 0, st, o, x, y, nvec, 0u); break;
+        default: return SOSX_ERR_ARG;
+    }
+    return hip_ok(hipGetLastError());
+}
 
 int sosxv_ping_split_launch(void *req, void *ans, long long idle_ticks, void *stream)
 {
