@@ -686,7 +686,48 @@ __global__ __launch_bounds__(kThreads) void k_stream(u32x4 *out, const u32x4 *a,
     }
 }
 
+// Multi-stream ceilings: R read streams, W write streams (1 or R), one vector per lane
+// per stream: W == 1 the fold's shape (xor of the R reads), W == R the prefix's (running
+// xor stored after each read), no arithmetic cost to speak of.
+struct StreamPtrs {
+    const u32x4 *in[8];
+    u32x4 *out[8];
+};
+
+template <int R, int W>
+__global__ __launch_bounds__(kThreads) void k_mstream(StreamPtrs p, size_t nvec)
+{
+    const size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= nvec) return;
+    u32x4 x[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) x[k] = __builtin_nontemporal_load(p.in[k] + i);
+    u32x4 acc = x[0];
+    if constexpr (W == R) __builtin_nontemporal_store(acc, p.out[0] + i);
+#pragma unroll
+    for (int k = 1; k < R; ++k) {
+        acc = acc ^ x[k];
+        if constexpr (W == R) __builtin_nontemporal_store(acc, p.out[k] + i);
+    }
+    if constexpr (W == 1) __builtin_nontemporal_store(acc, p.out[0] + i);
+}
+
 extern "C" {
+
+// 8 reads + 1 write (wide = 0) or 8 reads + 8 writes (wide = 1), under `lds` bytes of
+// unused dynamic LDS (the product's occupancy cap: 48 KiB -> 3, 64 KiB -> 2 per CU).
+int sosxv_mstream(int wide, void *const *outs, const void *const *ins, size_t nvec, unsigned lds, void *stream)
+{
+    StreamPtrs p;
+    for (int k = 0; k < 8; ++k) {
+        p.in[k] = (const u32x4 *)ins[k];
+        p.out[k] = (u32x4 *)outs[wide ? k : 0];
+    }
+    const unsigned blocks = (unsigned)((nvec + kThreads - 1) / kThreads);
+    if (wide) hipLaunchKernelGGL((k_mstream<8, 8>), dim3(blocks), dim3(kThreads), lds, as_stream(stream), p, nvec);
+    else hipLaunchKernelGGL((k_mstream<8, 1>), dim3(blocks), dim3(kThreads), lds, as_stream(stream), p, nvec);
+    return hip_ok(hipGetLastError());
+}
 
 // kind 0 read-only, 1 write-only, 2 copy, 3 two reads + one write; nvec 16-B vectors.
 int sosxv_stream(int kind, void *out, const void *a, const void *b, size_t nvec, void *stream)
