@@ -65,6 +65,8 @@ def main():
         # the fold's 9 and the prefix's 16 streams: bare streams (with and without the
         # product's occupancy cap) beside the product kernels, 16Mi fp32 per stream in 17
         # allocations 64 MiB + 4 KiB colour apart (the device heap's placement)
+        v.sosxv_fold_fast8.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint,
+                                       ctypes.c_void_p]
         v.sosxv_mstream.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint,
                                     ctypes.c_void_p]
         chunk = 16 << 20
@@ -79,6 +81,7 @@ def main():
         legs = {"bare 8 reads + 1 write": lambda: v.sosxv_mstream(0, one, ins, cb // 16, 0, st),
                 "bare 8 reads + 1 write, 3 per CU": lambda: v.sosxv_mstream(0, one, ins, cb // 16, 48 << 10, st),
                 "sosx_fold 8 inputs": lambda: L.fold(5, 23, 0, mp[16], mp[:8], chunk, st),
+                "fast-path fold 8 inputs, 3 per CU": lambda: v.sosxv_fold_fast8(mp[16], ins, chunk, 48 << 10, st),
                 "bare 8 reads + 8 writes": lambda: v.sosxv_mstream(1, outs, ins, cb // 16, 0, st),
                 "bare 8 reads + 8 writes, 2 per CU": lambda: v.sosxv_mstream(1, outs, ins, cb // 16, 64 << 10, st),
                 "sosx_prefix 8 inputs": lambda: L.prefix(5, 23, mp[8:16], mp[:8], chunk, -1, st)}

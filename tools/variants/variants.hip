@@ -686,6 +686,35 @@ __global__ __launch_bounds__(kThreads) void k_stream(u32x4 *out, const u32x4 *a,
     }
 }
 
+// The product's 8-input fp32-sum LINEAR fold with a fast path: the chain of plain IEEE
+// adds first; only when a lane of the wave ends in NaN, the exact chain with the x86 NaN
+// rules (bit-exact either way: NaN is absorbing for +).  Same tile shape and cap as
+// k_fold<float, OpSum, 8, LINEAR, 1>; the A/B of tools/stream_ceiling.py --multi.
+__global__ __launch_bounds__(kThreads) void k_fold_fast8(float *out, FoldPtrs ins, Geom g)
+{
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        u32x4 x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = ldv<true>(reinterpret_cast<const u32x4 *>((const float *)ins.p[k] + g.head) + i);
+        float r[4];
+        bool nan = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float acc = __builtin_bit_cast(float, x[0][j]);
+#pragma unroll
+            for (int k = 1; k < 8; ++k) acc = acc + __builtin_bit_cast(float, x[k][j]);
+            r[j] = acc;
+            nan |= __builtin_isnan(acc);
+        }
+        u32x4 v = {__builtin_bit_cast(unsigned, r[0]), __builtin_bit_cast(unsigned, r[1]),
+                   __builtin_bit_cast(unsigned, r[2]), __builtin_bit_cast(unsigned, r[3])};
+        if (__builtin_expect(__any(nan), 0)) v = fold_pack<float, OpSum, 8, SOSX_ORDER_LINEAR>(x);
+        stv<true>(O + i, v);
+    }
+}
+
 // Multi-stream ceilings: R read streams, W write streams (1 or R), one vector per lane
 // per stream: W == 1 the fold's shape (xor of the R reads), W == R the prefix's (running
 // xor stored after each read), no arithmetic cost to speak of.
@@ -726,6 +755,20 @@ int sosxv_mstream(int wide, void *const *outs, const void *const *ins, size_t nv
     const unsigned blocks = (unsigned)((nvec + kThreads - 1) / kThreads);
     if (wide) hipLaunchKernelGGL((k_mstream<8, 8>), dim3(blocks), dim3(kThreads), lds, as_stream(stream), p, nvec);
     else hipLaunchKernelGGL((k_mstream<8, 1>), dim3(blocks), dim3(kThreads), lds, as_stream(stream), p, nvec);
+    return hip_ok(hipGetLastError());
+}
+
+// The fast-path fold above over n fp32 elements (16-B aligned, n a multiple of 1024),
+// under `lds` bytes of unused dynamic LDS.
+int sosxv_fold_fast8(void *out, const void *const *ins, size_t n, unsigned lds, void *stream)
+{
+    FoldPtrs p;
+    memset(&p, 0, sizeof(p));
+    for (int k = 0; k < 8; ++k) p.p[k] = ins[k];
+    Geom g = make_geom((uintptr_t)out, n, sizeof(float), 1);
+    if (g.head || g.has_rem) return SOSX_ERR_ARG;
+    hipLaunchKernelGGL(k_fold_fast8, dim3(grid_for(g, kNoCap)), dim3(kThreads), lds, as_stream(stream),
+                       (float *)out, p, g);
     return hip_ok(hipGetLastError());
 }
 
