@@ -491,7 +491,8 @@ hipError_t release_system(hipStream_t stream)
 // The release event, then a stream synchronisation: it waits for the event too, and
 // costs what a plain hipStreamSynchronize does, 1.5-4.5 us less per call than waiting on
 // the event itself (profiles/r5_sync_cost.json).  Test build only: SOSX_TEST_EVENT_WAIT=1
-// waits with hipEventSynchronize, as round 5 first did (the A/B of DESIGN.md section 6.2).
+// waits with hipEventSynchronize, as round 5 first did (the A/B in
+// profiles/r5_p2p_small_call_ab.txt: 0.3-1 us per p2p call with two PEs on one GPU).
 hipError_t sync_system(hipStream_t stream)
 {
     hipError_t e = release_system(stream);
