@@ -61,6 +61,12 @@ struct SosxResidentDesc {
     long long limit;
 };
 
+#ifdef __cplusplus
+/* k_resident copies the descriptor one 8-byte word per lane of its 256-lane workgroup */
+static_assert(sizeof(struct SosxResidentDesc) % 8 == 0, "descriptor: whole 8-byte words");
+static_assert(sizeof(struct SosxResidentDesc) / 8 <= 256, "descriptor: one word per lane");
+#endif
+
 struct SosxResidentCtl {
     uint64_t req;
     uint64_t done;
