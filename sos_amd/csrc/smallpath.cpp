@@ -578,6 +578,19 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         g_strace.t[ph] += now - tp;
         tp = now;
     };
+    auto trace_end = [&]() {  // a call's phases into the window; print every `every` calls
+        if (!tr) return;
+        phase(5);
+        if (++g_strace.calls % g_strace.every == 0) {
+            const double k = 1e6 / (double)g_strace.every;
+            fprintf(stderr, "[%04d] small-path trace (calls %ld-%ld, us/call): slot %.2f copy+post %.2f "
+                    "peers %.2f launch %.2f done %.2f acks+out %.2f\n", s.my_pe,
+                    g_strace.calls - g_strace.every + 1, g_strace.calls, g_strace.t[0] * k,
+                    g_strace.t[1] * k, g_strace.t[2] * k, g_strace.t[3] * k, g_strace.t[4] * k,
+                    g_strace.t[5] * k);
+            for (double &v : g_strace.t) v = 0;
+        }
+    };
     // 1. my slot is free once every receiver of its previous post has read it
     for (const auto &u : g.slot_users[sl]) wait_ge(ctl(u.first)->consumed[mw].v, u.second, "a peer to read a slot");
     g.slot_users[sl].clear();
@@ -681,6 +694,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
             if (!direct) memcpy(target, g.out, bytes);
             g.calls++;
             g.dev_calls++;
+            trace_end();
             return;
         }
     } else if (staged) {
@@ -811,18 +825,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     if (!direct && out) memcpy(target, g.out, bytes);
     g.calls++;
     if (dev_src || dev_dst) g.dev_calls++;
-    if (tr) {
-        phase(5);
-        if (++g_strace.calls % g_strace.every == 0) {
-            const double k = 1e6 / (double)g_strace.every;
-            fprintf(stderr, "[%04d] small-path trace (calls %ld-%ld, us/call): slot %.2f copy+post %.2f "
-                    "peers %.2f launch %.2f done %.2f acks+out %.2f\n", s.my_pe,
-                    g_strace.calls - g_strace.every + 1, g_strace.calls, g_strace.t[0] * k,
-                    g_strace.t[1] * k, g_strace.t[2] * k, g_strace.t[3] * k, g_strace.t[4] * k,
-                    g_strace.t[5] * k);
-            for (double &v : g_strace.t) v = 0;
-        }
-    }
+    trace_end();
 }
 
 // ---------------------------------------------------------------------------------
