@@ -166,9 +166,11 @@ int sosx_small_ring(int op, int dtype, void *out, const void *const *ins, int np
 /* The LINEAR fold ((ins[0] OP ins[1]) OP ...) OP ins[np-1] of np = 1..8 operands in one
  * launch: one PE's team scan value (inscan: the team's sources 0..me, exscan 0..me-1,
  * src/collectives.c:1111-1209) on the small host-resident path.  Completion words as
- * sosx_small_fold. */
+ * sosx_small_fold.  acquire != 0: the operands are peers' slots, and every workgroup runs
+ * a system-scope acquire before its first load (as sosx_small_fold and sosx_small_ring
+ * always do); 0 for local operands. */
 int sosx_small_linear(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
-                      uint32_t *flags, uint32_t seq, int *nblocks, void *stream);
+                      uint32_t *flags, uint32_t seq, int *nblocks, int acquire, void *stream);
 
 /* Fill `count` elements of device buffer dst with the synthetic input of PE `pe`,
  * element indices [index0, index0 + count).  Bit-identical to the CPU generator
@@ -238,6 +240,22 @@ size_t sosx_release_workspaces(void);
  * call returns.  Introspection for tests. */
 long sosx_sys_releases(void);
 
+/* The consumer half of the memory-visibility rule: a launch that
+ * reads bytes a peer published (the p2p transport's gathers and in-place folds of peer
+ * memory, the small path's slot reads) follows, in stream order, a system-scope acquire
+ * issued after the wait for the peer's post.  *acquires: acquires issued (acquire
+ * kernels, and launches that carry their own per-workgroup acquire); *peer_reads:
+ * consuming launches; *unacquired: consuming launches with a peer wait since the last
+ * acquire (0 unless the protocol is broken); *xcc_mask: the XCDs the acquire kernels ran
+ * on (synchronises the library stream).  Any pointer may be null.  Introspection for
+ * tests. */
+void sosx_acquire_stats(long *acquires, long *peer_reads, long *unacquired, unsigned *xcc_mask);
+
+/* One acquire kernel on `stream`: 64 workgroups, each running a system-scope acquire
+ * (buffer_inv sc0 sc1: this CU's L1 and its XCD's L2 drop lines other agents may have
+ * rewritten) and OR-ing its XCD id into *xcc_mask (device memory, or null). */
+int sosx_acquire_system(unsigned *xcc_mask, void *stream);
+
 /* The p2p transport's mapping flags (introspection for tests): the hipHostRegister
  * flags of the shared pair-counter segment and the hipIpcOpenMemHandle flags of a peer's
  * device heap. */
@@ -256,10 +274,6 @@ int sosx_small_stage(void *dst, const void *src, size_t bytes, uint64_t *const *
 
 long sosx_small_path_calls(void);
 long sosx_small_path_device_calls(void);
-/* The resident small-path executor (SHMEMX_SMALL_RESIDENT=1, sos_amd/csrc/resident.h):
- * requests it served and kernel launches it took in this process. */
-long sosx_small_resident_calls(void);
-long sosx_small_resident_launches(void);
 /* Limit for device-resident operands on that path: a call takes it when team size *
  * operand bytes <= team_bytes (0: never; default SHMEMX_SMALL_DEVICE, 128 KiB).  Returns
  * the previous limit.  Collective in effect: every PE of a team must hold the same limit

@@ -78,7 +78,7 @@ _SIGS = {
                                    _c.c_void_p]),
     "sosx_small_linear": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _c.POINTER(_c.c_void_p), _c.c_int,
                                      _c.c_size_t, _c.c_void_p, _c.c_uint32, _c.POINTER(_c.c_int),
-                                     _c.c_void_p]),
+                                     _c.c_int, _c.c_void_p]),
     "sosx_fill": (_c.c_int, [_c.c_int, _c.c_int, _c.c_uint64, _c.c_int, _c.c_void_p,
                              _c.c_size_t, _c.c_size_t, _c.c_void_p]),
     "sosx_count_mismatch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_size_t,
@@ -89,8 +89,6 @@ _SIGS = {
     "sosx_build_info": (_c.c_char_p, []),
     "sosx_small_path_calls": (_c.c_long, []),
     "sosx_small_path_device_calls": (_c.c_long, []),
-    "sosx_small_resident_calls": (_c.c_long, []),
-    "sosx_small_resident_launches": (_c.c_long, []),
     "sosx_small_stage": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_void_p,
                                     _c.c_int, _c.c_void_p]),
     "sosx_set_small_device_bytes": (_c.c_size_t, [_c.c_size_t]),
@@ -101,6 +99,9 @@ _SIGS = {
     "sosx_rccl_comm_count": (_c.c_int, []),
     "sosx_release_workspaces": (_c.c_size_t, []),
     "sosx_sys_releases": (_c.c_long, []),
+    "sosx_acquire_stats": (None, [_c.POINTER(_c.c_long), _c.POINTER(_c.c_long), _c.POINTER(_c.c_long),
+                                  _c.POINTER(_c.c_uint)]),
+    "sosx_acquire_system": (_c.c_int, [_c.c_void_p, _c.c_void_p]),
     "sosx_gather": (_c.c_int, [_c.c_int, _c.POINTER(_c.c_void_p), _c.POINTER(_c.c_void_p),
                                _c.POINTER(_c.c_size_t), _c.c_void_p]),
 }

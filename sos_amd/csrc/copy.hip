@@ -65,6 +65,38 @@ using SigArgs = Sig<kMaxSig>;
 
 __global__ __launch_bounds__(kMaxSig) void k_p2p_signal(SigArgs a) { sig_step(a, threadIdx.x); }
 
+// ---------------------------------------------------------------------------------
+// The consumer half of the memory-visibility rule.  A peer's
+// bytes are read after a wait that saw its post; this GPU's L2s may still hold lines of
+// the same addresses from an earlier call, and a kernel dispatch does not promise to drop
+// them (tools/acquire_probe.hip: a kernel queued behind a device-side wait read a whole
+// rewritten buffer stale).  A system-scope acquire does: buffer_inv sc0 sc1 drops this
+// CU's L1 and the non-local lines of its XCD's L2.  Its cost rules out one per workgroup of
+// a streaming kernel (a 1 GiB copy 6.6 -> 1.1 TB/s, profiles/r6_acquire_probe.txt), so
+// the transport enqueues THIS kernel once per consuming step instead (+2.1 us): 64
+// one-wave workgroups, dealt round-robin over the 8 XCDs, each fencing and recording its
+// XCD id (the mask tests read).  The next launch on the stream starts after it completes.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void acquire_system_wg()
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: buffer_inv sc0 sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+constexpr unsigned kAcquireBlocks = 64;
+
+__global__ __launch_bounds__(64) void k_acquire_system(unsigned *xcc_mask)
+{
+    if (threadIdx.x == 0) {
+        acquire_system_wg();
+        if (xcc_mask) {
+            unsigned id;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(id));
+            atomicOr(xcc_mask, 1u << (id & 31u));
+        }
+    }
+}
+
 struct GatherArgs {
     const char *src[kMaxSeg];
     char *dst[kMaxSeg];
@@ -94,7 +126,15 @@ constexpr uint64_t kTileVec = (uint64_t)kThreads * kGatherU;
 template <bool GATED>
 __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g, Sig<kMaxGate> gate)
 {
-    if constexpr (GATED) sig_step(gate, threadIdx.x);
+    if constexpr (GATED) {
+        sig_step(gate, threadIdx.x);
+        // the awaited posts published peers' bytes: this workgroup's own acquire before
+        // its loads (at most kGateMaxBlocks workgroups, so the price is one invalidate each)
+        if (gate.nq > 0) {
+            if (threadIdx.x == 0) acquire_system_wg();
+            __syncthreads();
+        }
+    }
     const uint64_t t = blockIdx.x;
     if (t < g.tstart[g.nseg]) {
         int s = 0;
@@ -253,6 +293,14 @@ int sosx_gather_signalled(int nseg, const void *const *srcs, void *const *dsts,
     gate.err = err;
     gate.limit = limit_ticks;
     return gather_impl(nseg, srcs, dsts, bytes, &gate, as_stream(stream));
+}
+
+// A system-scope acquire in stream order (k_acquire_system above); xcc_mask: a device word
+// that collects the XCD ids it ran on, or null.
+int sosx_acquire_system(unsigned *xcc_mask, void *stream)
+{
+    hipLaunchKernelGGL(k_acquire_system, dim3(kAcquireBlocks), dim3(64), 0, as_stream(stream), xcc_mask);
+    return hip_ok(hipGetLastError());
 }
 
 // One signalling step of the p2p transport on `stream`: store vals[i] to waddr[i]

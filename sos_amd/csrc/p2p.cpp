@@ -372,7 +372,22 @@ namespace sosrt {
 
 namespace {
 
+// Does p lie in a peer's device heap as mapped here (bytes another PE published)?
+bool in_peer_heap(const void *p)
+{
+    const State &s = st();
+    for (size_t q = 0; q < s.peer_heap.size(); ++q) {
+        const char *b = s.peer_heap[q];
+        if ((int)q != s.my_pe && b && (const char *)p >= b && (const char *)p < b + s.dev_heap_bytes)
+            return true;
+    }
+    return false;
+}
+
 // The protocol's backend on this PE's HIP stream (p2p_proto.h), both signalling modes.
+// It classifies waits and launches itself for the consumer-side check (note_peer_wait /
+// note_peer_read, runtime.h): a wait on a `posted` / `dposted` counter is a wait for a
+// peer's bytes; a gather or fold reading a peer's heap is a peer read.
 struct HipBackend {
     hipStream_t stream;
     int op, dt;
@@ -382,8 +397,18 @@ struct HipBackend {
     int complete() { return sosrt::complete(stream) == hipSuccess ? 0 : 1; }
     int drain() { return hipStreamSynchronize(stream) == hipSuccess ? 0 : 1; }
     int release() { return release_system(stream) == hipSuccess ? 0 : 1; }
+    int acquire() { return acquire_system(stream) == hipSuccess ? 0 : 1; }
+    bool device_data_wait(int nq, const uint64_t *const *qa)
+    {
+        for (int i = 0; i < nq; ++i)
+            if (sosp2p::in_dposted(shared(), g_sig.dbase, qa[i])) return true;
+        return false;
+    }
     int gather(int n, const void *const *srcs, void *const *dsts, const size_t *bytes)
     {
+        bool peer = false;
+        for (int i = 0; i < n; ++i) peer |= in_peer_heap(srcs[i]);
+        if (peer) note_peer_read(false);
         prof_mark(1, false, stream);
         const int rc = sosx_gather(n, srcs, dsts, bytes, stream);
         prof_mark(1, true, stream);
@@ -392,6 +417,7 @@ struct HipBackend {
     int signal(int nw, uint64_t *const *wa, const uint64_t *wv, int nq, const uint64_t *const *qa,
                const uint64_t *qv)
     {
+        if (device_data_wait(nq, qa)) note_peer_wait();
         return sosx_p2p_signal(nw, wa, wv, nq, qa, qv, dev(&shared()->sig_err[my_world]),
                                g_sig.limit_ticks, stream);
     }
@@ -399,6 +425,13 @@ struct HipBackend {
                          uint64_t *const *wa, const uint64_t *wv, int nq, const uint64_t *const *qa,
                          const uint64_t *qv)
     {
+        // the step's waits run inside the launch; with a wait for peers' bytes every
+        // workgroup acquires before its loads (copy.hip k_gather<true>)
+        const bool own = device_data_wait(nq, qa);
+        if (own) note_peer_wait();
+        bool peer = false;
+        for (int i = 0; i < n; ++i) peer |= in_peer_heap(srcs[i]);
+        if (peer) note_peer_read(own);
         prof_mark(1, false, stream);
         const int rc = sosx_gather_signalled(n, srcs, dsts, bytes, nw, wa, wv, nq, qa, qv,
                                              dev(&shared()->sig_err[my_world]), g_sig.limit_ticks, stream);
@@ -408,13 +441,26 @@ struct HipBackend {
     int run_ops(const sosplan::Round &r, const std::vector<std::vector<const void *>> &ins,
                 const sosp2p::LocalPtr &local_ptr)
     {
+        for (const auto &in : ins) {
+            bool peer = false;
+            for (const void *p : in) peer |= in_peer_heap(p);
+            if (peer) note_peer_read(false);
+        }
         return run_round_ops(r, ins, local_ptr, op, dt, stream);
     }
     uint64_t *dev(uint64_t *p) { return sosrt::dev(p); }
     const uint64_t *dev(const uint64_t *p) { return sosrt::dev(p); }
     const char *peer_base(int pw) { return st().peer_heap[(size_t)pw]; }
-    void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what) { spin_until(a, want, what); }
-    void spin_u64(const uint64_t *a, uint64_t want, const char *what) { spin_until_u64(a, want, what); }
+    void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what)
+    {
+        spin_until(a, want, what);
+        if (sosp2p::in_posted(shared(), &a)) note_peer_wait();
+    }
+    void spin_u64(const uint64_t *a, uint64_t want, const char *what)
+    {
+        spin_until_u64(a, want, what);
+        if (sosp2p::in_dposted(shared(), (const char *)shared(), a)) note_peer_wait();
+    }
     void entry_hook() { stall_hook(); }
     bool host_entry() { return g_sig.host_entry; }
     bool device_wait_failed()

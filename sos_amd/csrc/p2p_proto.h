@@ -16,6 +16,13 @@
 //   4. complete the stream, mark every receive consumed (consumed[from][me]++, release),
 //      wait until every peer consumed this PE's sends (acquire); then the round's
 //      remaining (non-fused) ops.
+// The consumer half of the memory-visibility rule: every launch
+// that reads a peer's bytes follows, in stream order, a system-scope acquire issued after
+// the wait that saw the peer's post (be.acquire(), or the gather that carries its own
+// signalling step and acquires in each of its workgroups).  Both backends check it on
+// their own: they classify each wait by the counter it reads and each launch by the
+// addresses it reads, and count a peer read with a wait since the last acquire as an
+// error (AcquireTrack; the HIP backend's counters are sosx_acquire_stats).
 // Only headers that need no HIP: plan.h (the plans) and <atomic>.
 #pragma once
 #include <stdint.h>
@@ -58,6 +65,41 @@ struct Shared {
     // free team-slot bit mask and the creation status, read by the other members
     std::atomic<uint64_t> team_word[2][kMaxPE];
 };
+
+// The consumer-side check, in stream (= enqueue) order: waited() when a wait for a peer's
+// post completes (host) or is queued (device step); acquired() for an acquire step;
+// read(own) for a launch that reads peer bytes (own: it acquires in every workgroup itself).
+struct AcquireTrack {
+    bool pending = false;
+    long acquires = 0, reads = 0, unacquired = 0;
+    void waited() { pending = true; }
+    void acquired()
+    {
+        pending = false;
+        ++acquires;
+    }
+    void read(bool own)
+    {
+        ++reads;
+        if (own) ++acquires;
+        else if (pending) ++unacquired;
+    }
+};
+
+inline bool in_posted(const Shared *sh, const void *p)
+{
+    const char *a = (const char *)&sh->posted[0][0], *b = (const char *)(&sh->posted[kMaxPE - 1][kMaxPE - 1] + 1);
+    return (const char *)p >= a && (const char *)p < b;
+}
+
+// dposted as seen through `base` (the host segment, or the device view of it: base is
+// where the segment starts in that view)
+inline bool in_dposted(const Shared *sh, const char *base, const void *p)
+{
+    const size_t a = (size_t)((const char *)&sh->dposted[0][0] - (const char *)sh);
+    const size_t b = (size_t)((const char *)(&sh->dposted[kMaxPE - 1][kMaxPE - 1] + 1) - (const char *)sh);
+    return (const char *)p >= base + a && (const char *)p < base + b;
+}
 
 // What one PE has seen/done per ordered pair (monotonic across calls).
 struct Local {
@@ -144,6 +186,7 @@ inline bool round_fusable(const sosplan::Round &r, uint64_t ts, const LocalPtr &
 //   int drain()           drain the stream (this PE's reads are done); 0 = ok
 //   int gather(n, srcs, dsts, bytes)                      one multi-segment copy
 //   int run_ops(round, ins, local_ptr)                    the round's local ops
+//   int acquire()          a system-scope acquire in stream order (before peer reads)
 //   const char *peer_base(world_pe)                       the peer's heap, mapped here
 //   void spin(std::atomic<uint64_t> &a, uint64_t want, const char *what)   bounded wait
 //   void plan_mismatch(world_pe)                          fatal
@@ -223,6 +266,8 @@ int exec_host(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of,
                 gd.push_back(sg.dst);
                 gb.push_back(sg.bytes);
             }
+        // the peers' posts were seen: acquire before the first launch that reads their bytes
+        if (!segs.empty() && be.acquire() != 0) return SOSX_ERR_HIP;
         if (!gs.empty()) {
             const int rc = be.gather((int)gs.size(), gs.data(), gd.data(), gb.data());
             if (rc) return rc;
@@ -306,8 +351,10 @@ int exec_stream(const sosplan::Plan &plan, int P, int me, const WorldOf &world_o
     // when no local op sits between them)
     std::map<uint64_t *, uint64_t> pw_store;
     std::map<const uint64_t *, uint64_t> pw_wait;
+    bool data_wait = false;  // pw_wait holds a wait for a peer's post (not only consumed marks)
     auto take = [&](std::vector<uint64_t *> &wa, std::vector<uint64_t> &wv,
                     std::vector<const uint64_t *> &qa, std::vector<uint64_t> &qv) {
+        data_wait = false;
         for (auto &kv : pw_store) {
             wa.push_back(be.dev(kv.first));
             wv.push_back(kv.second);
@@ -324,12 +371,16 @@ int exec_stream(const sosplan::Plan &plan, int P, int me, const WorldOf &world_o
         // posts make the bytes of this round's sends readable by peers, on other GPUs
         // over xGMI: a system-scope release in stream order first
         if (!pw_store.empty() && be.release() != 0) return SOSX_ERR_HIP;
+        const bool acq = data_wait;
         std::vector<uint64_t *> wa;
         std::vector<uint64_t> wv;
         std::vector<const uint64_t *> qa;
         std::vector<uint64_t> qv;
         take(wa, wv, qa, qv);
-        return be.signal((int)wa.size(), wa.data(), wv.data(), (int)qa.size(), qa.data(), qv.data());
+        const int rc = be.signal((int)wa.size(), wa.data(), wv.data(), (int)qa.size(), qa.data(), qv.data());
+        if (rc) return rc;
+        // the step awaited peers' posts: the acquire before anything reads their bytes
+        return acq && be.acquire() != 0 ? SOSX_ERR_HIP : SOSX_OK;
     };
     // the same step done by the host (the call's first and last boundaries)
     auto host_flush = [&]() {
@@ -337,6 +388,7 @@ int exec_stream(const sosplan::Plan &plan, int P, int me, const WorldOf &world_o
         for (auto &kv : pw_wait) be.spin_u64(kv.first, kv.second, "a peer (call boundary)");
         pw_store.clear();
         pw_wait.clear();
+        data_wait = false;
     };
     std::vector<int> recv_idx((size_t)P, 0);  // k-th receive from each team peer
     bool first_xfer_round = true;
@@ -356,8 +408,12 @@ int exec_stream(const sosplan::Plan &plan, int P, int me, const WorldOf &world_o
         // peers' posts of what this round receives
         for (const auto &x : r.xfers) {
             const int pw = world_of(x.peer);
-            if (x.send) pw_store[&sh->dposted[my_world][pw]] = ++sl.posted[pw];
-            else pw_wait[&sh->dposted[pw][my_world]] = ++sl.seen[pw];
+            if (x.send) {
+                pw_store[&sh->dposted[my_world][pw]] = ++sl.posted[pw];
+            } else {
+                pw_wait[&sh->dposted[pw][my_world]] = ++sl.seen[pw];
+                data_wait = true;
+            }
         }
         int rc;
         bool step_pending = false;  // the signalling step still to be enqueued
@@ -375,7 +431,9 @@ int exec_stream(const sosplan::Plan &plan, int P, int me, const WorldOf &world_o
             bool sends = false;
             for (const auto &x : r.xfers) sends |= x.send != 0;
             if (sends && be.complete() != 0) return SOSX_ERR_HIP;
+            const bool acq = data_wait;
             host_flush();
+            if (acq && be.acquire() != 0) return SOSX_ERR_HIP;
             be.entry_hook();
         } else {
             step_pending = true;
@@ -431,6 +489,11 @@ int exec_stream(const sosplan::Plan &plan, int P, int me, const WorldOf &world_o
             rc = be.gather_signalled((int)gs.size(), gs.data(), gd.data(), gb.data(), (int)wa.size(),
                                      wa.data(), wv.data(), (int)qa.size(), qa.data(), qv.data());
             if (rc) return rc;
+            // the gather's workgroups acquired for their own loads only: folds below that
+            // read peer bytes in place need the stream-wide acquire
+            bool peer_ops = false;
+            for (const auto &sg : segs) peer_ops |= sg.used;
+            if (fuse_ok && peer_ops && be.acquire() != 0) return SOSX_ERR_HIP;
         } else {
             if (step_pending) {
                 rc = flush();

@@ -488,6 +488,29 @@ hipError_t release_system(hipStream_t stream)
     return hipEventRecord(s.sys_ev, stream);
 }
 
+hipError_t acquire_system(hipStream_t stream)
+{
+    State &s = st();
+    if (!s.acq_mask) {
+        hipError_t e = hipMalloc(&s.acq_mask, sizeof(unsigned));
+        if (e == hipSuccess) e = hipMemsetAsync(s.acq_mask, 0, sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
+    }
+    ++s.sys_acquires;
+    s.acq_pending = false;
+    return sosx_acquire_system(s.acq_mask, stream) == SOSX_OK ? hipSuccess : hipErrorLaunchFailure;
+}
+
+void note_peer_wait() { st().acq_pending = true; }
+
+void note_peer_read(bool own_acquire)
+{
+    State &s = st();
+    ++s.peer_reads;
+    if (own_acquire) ++s.sys_acquires;
+    else if (s.acq_pending) ++s.peer_reads_unacquired;
+}
+
 // The release event, then a stream synchronisation: it waits for the event too, and
 // costs what a plain hipStreamSynchronize does, 1.5-4.5 us less per call than waiting on
 // the event itself (profiles/r5_sync_cost.json).  Test build only: SOSX_TEST_EVENT_WAIT=1
@@ -814,6 +837,8 @@ void shmem_finalize(void)
         }
     if (s.sys_ev) (void)hipEventDestroy(s.sys_ev);
     s.sys_ev = nullptr;
+    if (s.acq_mask) (void)hipFree(s.acq_mask);
+    s.acq_mask = nullptr;
     for (hipStream_t *ps : {&s.pipe_h2d, &s.pipe_d2h}) {
         if (*ps) (void)hipStreamDestroy(*ps);
         *ps = nullptr;
@@ -1045,6 +1070,19 @@ int sosx_rccl_comm_count(void)
 // How many system-scope completion markers (sync_system / release_system) this PE has
 // issued: every call that returns data ends with one (introspection for tests).
 long sosx_sys_releases(void) { return st().sys_releases; }
+
+void sosx_acquire_stats(long *acquires, long *peer_reads, long *unacquired, unsigned *xcc_mask)
+{
+    State &s = st();
+    if (acquires) *acquires = s.sys_acquires;
+    if (peer_reads) *peer_reads = s.peer_reads;
+    if (unacquired) *unacquired = s.peer_reads_unacquired;
+    if (xcc_mask) {
+        *xcc_mask = 0;
+        if (s.acq_mask && s.stream && hipStreamSynchronize(s.stream) == hipSuccess)
+            (void)hipMemcpy(xcc_mask, s.acq_mask, sizeof(unsigned), hipMemcpyDeviceToHost);
+    }
+}
 
 // Return this PE's private device workspaces (exchange scratch, staging for host
 // operands) to the runtime after the library stream drains; the next call that needs one

@@ -87,6 +87,10 @@ struct State {
     hipEvent_t pipe_ev[3][3] = {};    // [slot][h2d done, exchange done, d2h done]
     hipEvent_t sys_ev = nullptr;      // system-scope release marker (sync_system)
     long sys_releases = 0;            // how many sync_system / release_system markers ran
+    // consumer half of the visibility rule (acquire_system, note_peer_wait/read)
+    long sys_acquires = 0, peer_reads = 0, peer_reads_unacquired = 0;
+    bool acq_pending = false;         // a peer wait since the last acquire (stream order)
+    unsigned *acq_mask = nullptr;     // device word: XCD ids the acquire kernels ran on
     void *stripes = nullptr;
     size_t stripes_bytes = 0;
     size_t host_stripe_bytes = 256u << 10; // SHMEMX_HOST_STRIPE_BYTES: min slice (0 = off)
@@ -158,6 +162,20 @@ hipError_t sync_system(hipStream_t stream);
 // The same release in stream order, without a host wait (stream-mode p2p posts).
 hipError_t release_system(hipStream_t stream);
 
+// The consumer half: a launch that reads bytes a peer published
+// must follow, in stream order, a system-scope acquire issued after the wait that saw the
+// peer's post.  A kernel dispatch does not promise one (tools/acquire_probe.hip: a
+// kernel queued behind a device-side wait read every line of a rewritten buffer stale,
+// and an acquire between the two removed it).  acquire_system enqueues the acquire kernel
+// (sosx_acquire_system) and clears the pending wait; note_peer_wait records a wait for a
+// peer's post (host spin or queued device wait); note_peer_read counts a consuming launch
+// -- own_acquire: the launch runs its own per-workgroup acquire (the small path, the
+// p2p gather that carries its signalling step) -- and flags one that follows a wait with
+// no acquire in between.  Counters: sosx_acquire_stats.
+hipError_t acquire_system(hipStream_t stream);
+void note_peer_wait();
+void note_peer_read(bool own_acquire);
+
 // Device workspaces (grown, never shrunk).
 void *scratch(size_t bytes);
 void *stage(size_t bytes);
@@ -210,8 +228,6 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
                        const Team &t, int op, int dt, const char *fn);
 long small_path_calls();
 long small_path_device_calls();
-long small_resident_calls();    // requests served by the resident executor
-long small_resident_launches(); // its launches (first use, relaunch after an idle exit)
 size_t small_path_set_device_bytes(size_t team_bytes);
 // shmemx_reduce_local on operands of <= 64 KiB that are both in HBM or both in host memory:
 // one launch + completion words (smallpath.cpp); false = not taken, use the general path.

@@ -13,8 +13,14 @@
 // stream synchronisation: every lane fences its stores at system scope and each
 // workgroup then stores the call's sequence number into its own word of pinned host
 // memory, which the host polls.
+//
+// The consumer half of the memory-visibility rule: the host
+// launches these kernels after it saw the peers' posts, and a kernel dispatch does not
+// promise to drop the lines an earlier call left in this GPU's L2s (tools/acquire_probe.hip,
+// profiles/r6_acquire_probe.txt).  So each workgroup of a kernel that reads the peers'
+// slots starts with a system-scope acquire (slot_acquire): lane 0 fences, waits for the
+// invalidate, and the workgroup's loads follow the barrier.
 #include "fold_kernels.h"
-#include "resident.h"
 
 namespace sos {
 
@@ -25,6 +31,15 @@ namespace sos {
 // MAXP = 8 for the P2 <= 8 kernels (one PE per GPU on a node): 150 B of kernel
 // arguments instead of 1 KiB, which the host launch call copies every time
 // (SOSX_SMALL_TRACE measured the launch call at 3.0 us with the 1 KiB block).
+__device__ __forceinline__ void slot_acquire()
+{
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: buffer_inv sc0 sc1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
 template <int MAXP> struct SmallFoldArgsT {
     const void *leaf[MAXP];
     const void *extra[MAXP];           // null: the leaf has no extra PE
@@ -91,7 +106,7 @@ __device__ __forceinline__ void store_pack(T *out, size_t i0, const Pack<T> &r, 
 
 // VEC: lane L handles elements [L*V, L*V + V) as 16-B vectors (every leaf/extra 16-B
 // aligned); the last, partial vector goes element by element.  Otherwise one element per
-// lane.  (One lane's share: k_small_fold and the resident executor below.)
+// lane.  (One lane's share: k_small_fold.)
 template <class T, class OP, int P2, bool VEC, class A>
 __device__ __forceinline__ void small_fold_lane(T *out, const A &a, size_t n, size_t lane)
 {
@@ -128,6 +143,7 @@ __device__ __forceinline__ void small_fold_lane(T *out, const A &a, size_t n, si
 template <class T, class OP, int P2, bool VEC, class A>
 __global__ __launch_bounds__(kThreads) void k_small_fold(T *out, A a, size_t n)
 {
+    slot_acquire();
     small_fold_lane<T, OP, P2, VEC, A>(out, a, n, (size_t)blockIdx.x * kThreads + threadIdx.x);
     signal_done(a.flags, a.seq);
 }
@@ -147,6 +163,7 @@ struct SmallRingArgs {
     uint32_t *flags;
     uint32_t seq;
     int vec_out;
+    int acquire;          // the operands are peers' slots: slot_acquire first
 };
 
 template <class T, class OP, int NP>
@@ -165,6 +182,7 @@ __device__ __forceinline__ T ring_elem(const SmallRingArgs &a, int c, size_t i)
 template <class T, class OP>
 __global__ __launch_bounds__(kThreads) void k_small_ring_dyn(T *out, SmallRingArgs a, int np)
 {
+    if (a.acquire) slot_acquire();
     const uint64_t b = blockIdx.x;
     int c = 0;
     while (b >= a.tstart[c + 1]) ++c;
@@ -184,6 +202,7 @@ __global__ __launch_bounds__(kThreads) void k_small_ring_dyn(T *out, SmallRingAr
 template <class T, class OP, int NP, bool VEC>
 __global__ __launch_bounds__(kThreads) void k_small_ring(T *out, SmallRingArgs a)
 {
+    if (a.acquire) slot_acquire();
     const uint64_t b = blockIdx.x;
     int c = 0;
     while (b >= a.tstart[c + 1]) ++c;
@@ -256,202 +275,6 @@ __global__ __launch_bounds__(kStageThreads) void k_small_stage(A a)
     __syncthreads();
     if ((int)threadIdx.x < a.nwords)
         __hip_atomic_store(a.word[threadIdx.x], a.val[threadIdx.x], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// ---------------------------------------------------------------------------------
-// The resident executor (resident.h): one workgroup that stays on the GPU and serves the
-// small path's requests from pinned host memory, so a call costs a request/answer round
-// trip instead of a launch and its completion wait.  Thread 0 polls; the workgroup
-// computes the request as k_small_fold / the single-chunk k_small_ring would, lane by
-// lane, fences at system scope and answers.  Every wave leaves the loop on `stop` or
-// after `idle_ticks` without a request.
-// ---------------------------------------------------------------------------------
-template <class T, class OP>
-__device__ __forceinline__ void resident_fold(const SosxResidentDesc &d)
-{
-    SmallFoldArgsT<8> a;
-#pragma unroll
-    for (int y = 0; y < 8; ++y) {
-        a.leaf[y] = d.in[y];
-        a.extra[y] = d.extra[y];
-    }
-    a.flags = nullptr;
-    a.seq = 0;
-    a.p2 = (int)d.np;
-    a.vec_out = 1;
-    T *out = (T *)d.out;
-    const size_t n = d.count;
-    if (d.vec) {
-        constexpr int V = Pack<T>::N;
-        const size_t lanes = (n + V - 1) / V;
-        switch (d.np) {
-#define SOS_RESIDENT_FOLD(P2)                                                          \
-    case P2:                                                                           \
-        for (size_t l = threadIdx.x; l < lanes; l += kThreads)                         \
-            small_fold_lane<T, OP, P2, true, SmallFoldArgsT<8>>(out, a, n, l);         \
-        break;
-            SOS_RESIDENT_FOLD(1)
-            SOS_RESIDENT_FOLD(2)
-            SOS_RESIDENT_FOLD(4)
-            SOS_RESIDENT_FOLD(8)
-#undef SOS_RESIDENT_FOLD
-        }
-    } else {
-        for (size_t l = threadIdx.x; l < n; l += kThreads)
-            small_fold_lane<T, OP, 0, false, SmallFoldArgsT<8>>(out, a, n, l);
-    }
-}
-
-template <class T, class OP>
-__device__ __forceinline__ void resident_linear(const SosxResidentDesc &d)
-{
-    T *out = (T *)d.out;
-    const size_t n = d.count;
-    const int np = (int)d.np;
-    size_t done = 0;
-    if (d.vec) {
-        constexpr int V = Pack<T>::N;
-        const size_t nv = n / V;
-        for (size_t l = threadIdx.x; l < nv; l += kThreads) {
-            u32x4 x[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (k < np) x[k] = reinterpret_cast<const u32x4 *>(d.in[k])[l];
-            u32x4 acc = x[0];
-#pragma unroll
-            for (int k = 1; k < 8; ++k)
-                if (k < np) acc = apply<T, OP>(acc, x[k]);
-            reinterpret_cast<u32x4 *>(out)[l] = acc;
-        }
-        done = nv * V;
-    }
-    for (size_t i = done + threadIdx.x; i < n; i += kThreads) {
-        T acc = ((const T *)d.in[0])[i];
-        for (int k = 1; k < np; ++k) acc = OP::f(acc, ((const T *)d.in[k])[i]);
-        out[i] = acc;
-    }
-}
-
-// k_small_stage's work in the resident workgroup: the operand's bytes into the slot, a
-// system-scope fence by every lane, then the posts (one lane each, after the barrier).
-__device__ __forceinline__ void resident_stage(const SosxResidentDesc &d)
-{
-    const uint8_t *s = (const uint8_t *)d.stage_src;
-    uint8_t *o = (uint8_t *)d.stage_dst;
-    uint64_t done = 0;
-    if (d.stage_vec) {
-        const uint64_t nv = d.stage_bytes / 16;
-        for (uint64_t i = threadIdx.x; i < nv; i += kThreads)
-            reinterpret_cast<u32x4 *>(o)[i] = reinterpret_cast<const u32x4 *>(s)[i];
-        done = nv * 16;
-    }
-    for (uint64_t i = done + threadIdx.x; i < d.stage_bytes; i += kThreads) o[i] = s[i];
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x < d.nposts)
-        __hip_atomic_store(d.post_word[threadIdx.x], d.post_val[threadIdx.x], __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// STAGE_FOLD after the staging: lane i < npeers waits for team member i's post (bounded:
-// on expiry it flags *err, and the fold is skipped), reads the slot id it posted in and
-// resolves its operand; then the leaves of the fold are taken from those operands.
-// Returns false when a wait expired.
-__device__ __forceinline__ bool resident_gather_slots(SosxResidentDesc &d, SosxResidentCtl *c)
-{
-    __shared__ const void *opnd[8];
-    __shared__ int expired;
-    if (threadIdx.x == 0) expired = 0;
-    __syncthreads();
-    const unsigned i = threadIdx.x;
-    if (i < d.npeers) {
-        if (!d.wait_word[i]) {
-            opnd[i] = d.slot[i][0];
-        } else {
-            const long long t0 = wall_clock64();
-            bool ok = true;
-            while (__hip_atomic_load(d.wait_word[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < d.wait_val[i]) {
-                if (wall_clock64() - t0 > d.limit) {
-                    ok = false;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (ok) {
-                const uint32_t r = __hip_atomic_load(d.ring_word[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                opnd[i] = d.slot[i][r & 1];
-            } else {
-                expired = 1;
-                __hip_atomic_store(&c->err, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-    }
-    __syncthreads();
-    if (expired) return false;
-    // the peers' slot bytes after their posts: every lane acquires before its loads
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    if (threadIdx.x == 0) {
-        for (unsigned y = 0; y < d.np; ++y) {
-            d.in[y] = opnd[d.leaf_idx[y]];
-            d.extra[y] = d.extra_idx[y] >= 0 ? opnd[d.extra_idx[y]] : nullptr;
-        }
-    }
-    __syncthreads();
-    return true;
-}
-
-template <class T, class OP>
-__global__ __launch_bounds__(kThreads) void k_resident(SosxResidentCtl *c, long long idle_ticks)
-{
-    __shared__ SosxResidentDesc sd;
-    __shared__ int cmd;
-    __shared__ uint64_t cur;
-    uint64_t last = 0;
-    if (threadIdx.x == 0) last = __hip_atomic_load(&c->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-    while (true) {
-        if (threadIdx.x == 0) {
-            int k = 0;  // 0: leave, 1: a request
-            const long long t0 = wall_clock64();
-            while (true) {
-                const uint64_t r = __hip_atomic_load(&c->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (r > last) {
-                    last = r;
-                    k = 1;
-                    break;
-                }
-                if (__hip_atomic_load(&c->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-                if (wall_clock64() - t0 > idle_ticks) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            cmd = k;
-            cur = last;
-        }
-        __syncthreads();
-        if (cmd == 0) break;
-        // every lane's loads of this request after thread 0's acquire: drop what the
-        // CU's caches hold from an earlier request at the same addresses
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        // the descriptor, one word per lane (one host-link round trip, not one per word)
-        constexpr unsigned kDescWords = sizeof(SosxResidentDesc) / 8;
-        if (threadIdx.x < kDescWords)
-            reinterpret_cast<uint64_t *>(&sd)[threadIdx.x] = __hip_atomic_load(
-                reinterpret_cast<const uint64_t *>(&c->d) + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __syncthreads();
-        if (sd.kind == SOSX_RESIDENT_FOLD) {
-            resident_fold<T, OP>(sd);
-        } else if (sd.kind == SOSX_RESIDENT_STAGE) {
-            resident_stage(sd);
-        } else if (sd.kind == SOSX_RESIDENT_STAGE_FOLD) {
-            resident_stage(sd);
-            if (resident_gather_slots(sd, c)) resident_fold<T, OP>(sd);
-        } else {
-            resident_linear<T, OP>(sd);
-        }
-        __threadfence_system();
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(&c->done, cur, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (threadIdx.x == 0) __hip_atomic_store(&c->exited, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace sos
@@ -531,15 +354,6 @@ struct SmallRingFn {
 };
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
-
-struct ResidentFn {
-    template <class T, class OP>
-    static int run(SosxResidentCtl *ctl, long long idle_ticks, hipStream_t st)
-    {
-        hipLaunchKernelGGL((k_resident<T, OP>), dim3(1), dim3(kThreads), 0, st, ctl, idle_ticks);
-        return hip_ok(hipGetLastError());
-    }
-};
 
 }  // namespace
 
@@ -624,6 +438,7 @@ int sosx_small_ring(int op, int dtype, void *out, const void *const *ins, int np
     a.flags = flags;
     a.seq = seq;
     a.vec_out = aligned16(out);
+    a.acquire = 1;
     *nblocks = (int)tiles;
     return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles,
                                  as_stream(stream));
@@ -632,9 +447,11 @@ int sosx_small_ring(int op, int dtype, void *out, const void *const *ins, int np
 // The LINEAR fold ((ins[0] OP ins[1]) OP ...) OP ins[np-1] of every element (np = 1..8:
 // the team scans' value at one PE, src/collectives.c:1111-1209 -- inscan folds the team's
 // sources 0..me, exscan 0..me-1), written to `out`; completion words as above.  This is
-// the ring kernel with a single chunk: every workgroup folds from ins[0].
+// the ring kernel with a single chunk: every workgroup folds from ins[0].  acquire != 0:
+// the operands are peers' slots (team calls), each workgroup acquires first; 0 for local
+// operands (shmemx_reduce_local).
 int sosx_small_linear(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
-                      uint32_t *flags, uint32_t seq, int *nblocks, void *stream)
+                      uint32_t *flags, uint32_t seq, int *nblocks, int acquire, void *stream)
 {
     if (np < 1 || np > 8 || count > SOSX_SMALL_FOLD_MAX || !flags || !nblocks) return SOSX_ERR_ARG;
     int rc = sos_check_op(op, dtype);
@@ -663,16 +480,10 @@ int sosx_small_linear(int op, int dtype, void *out, const void *const *ins, int 
     a.flags = flags;
     a.seq = seq;
     a.vec_out = aligned16(out);
+    a.acquire = acquire != 0;
     *nblocks = (int)tiles;
     return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles,
                                  as_stream(stream));
-}
-
-// The resident executor of (op, dtype) over `ctl` (resident.h), one workgroup on `stream`.
-int sosx_resident_launch(int op, int dtype, SosxResidentCtl *ctl, long long idle_ticks, void *stream)
-{
-    if (!ctl || idle_ticks <= 0) return SOSX_ERR_ARG;
-    return dispatch<ResidentFn>(op, dtype, ctl, idle_ticks, as_stream(stream));
 }
 
 // Copy `bytes` from src (device) to dst (a node-shared slot, device view) in one

@@ -38,10 +38,11 @@
 // over the host link costs as much as the exchange saves, or more.  The path takes device
 // operands while P * bytes <= SHMEMX_SMALL_DEVICE (default 128 KiB).  The GPU-side posts
 // do not shorten the critical path (a peer's fold still launches after the post arrives);
-// they save the host a completion round trip.  With SHMEMX_SMALL_RESIDENT=1 (resident.h)
-// calls up to 4 KiB per operand run as requests to a resident kernel instead of launches;
-// a device operand's recdbl_sw call is then ONE request: staging, posts, the waits for
-// the peers' posts (on the device, bounded) and the fold.
+// they save the host a completion round trip.
+//
+// Memory visibility, consumer side: every kernel that reads the
+// peers' slots runs a system-scope acquire in each workgroup before its first slot load
+// (small.hip slot_acquire), after the host saw the peers' posts.
 //
 // Slot reuse: each PE alternates between two data slots.  A post to receiver r carries
 // a per-pair index k (posted[q][r] = k) and the slot id (ring[q][r][k % 2]); receiver r
@@ -61,7 +62,6 @@
 #include <vector>
 
 #include "plan.h"
-#include "resident.h"
 #include "runtime.h"
 #include "sosx.h"
 
@@ -219,125 +219,6 @@ struct SmallTrace {
 };
 SmallTrace g_strace;
 
-// ---------------------------------------------------------------------------------
-// The resident executor (resident.h; opt-in SHMEMX_SMALL_RESIDENT=1): one kernel per
-// (op, type) in use, each on a stream of its own, serving requests from pinned words.
-// ---------------------------------------------------------------------------------
-struct Resident {
-    SosxResidentCtl *ctl = nullptr;  // pinned, coherent (the same address on the device)
-    hipStream_t stream = nullptr;
-    bool running = false;
-    uint64_t seq = 0;
-};
-struct ResidentSet {
-    int on = -1;  // -1: SHMEMX_SMALL_RESIDENT not read yet
-    long long idle_ticks = 0;
-    std::map<int, Resident> by_key;  // op * 256 + dtype
-    long calls = 0, launches = 0;
-    int khz = 0;                     // device wall clock (kHz)
-};
-ResidentSet g_res;
-
-bool resident_on()
-{
-    if (g_res.on < 0) {
-        const char *e = getenv("SHMEMX_SMALL_RESIDENT");
-        g_res.on = e && *e == '1' ? 1 : 0;
-        const char *ie = getenv("SHMEMX_SMALL_RESIDENT_IDLE_US");
-        const double idle_us = ie && *ie ? atof(ie) : 2000.0;
-        int khz = 0;
-        if (g_res.on && (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, st().device) != hipSuccess ||
-                         khz <= 0)) {
-            (void)hipGetLastError();
-            g_res.on = 0;
-        }
-        g_res.khz = khz;
-        g_res.idle_ticks = (long long)((idle_us > 0 ? idle_us : 2000.0) * 1e-3 * (double)khz);
-        if (g_res.idle_ticks < 1) g_res.idle_ticks = 1;
-    }
-    return g_res.on == 1;
-}
-
-// The executor of (op, dt), created on first use; null if HIP refuses the resources.
-Resident *resident_get(int op, int dt)
-{
-    Resident &R = g_res.by_key[op * 256 + dt];
-    if (R.ctl) return &R;
-    if (hipHostMalloc((void **)&R.ctl, sizeof(SosxResidentCtl), hipHostMallocCoherent) != hipSuccess ||
-        hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking) != hipSuccess) {
-        (void)hipGetLastError();
-        if (R.ctl) (void)hipHostFree(R.ctl);
-        g_res.by_key.erase(op * 256 + dt);
-        return nullptr;
-    }
-    memset((void *)R.ctl, 0, sizeof(SosxResidentCtl));
-    return &R;
-}
-
-void resident_launch(Resident &R, int op, int dt, const char *fn)
-{
-    if (R.running) hip_check(hipStreamSynchronize(R.stream), fn);  // the previous one has exited
-    __atomic_store_n(&R.ctl->exited, (uint64_t)0, __ATOMIC_RELAXED);
-    __atomic_store_n(&R.ctl->stop, (uint64_t)0, __ATOMIC_RELEASE);
-    const int rc = sosx_resident_launch(op, dt, R.ctl, g_res.idle_ticks, R.stream);
-    if (rc) raise_error("%s: resident small-path executor launch failed (status %d)", fn, rc);
-    R.running = true;
-    g_res.launches++;
-}
-
-// Run one request on the executor of (op, dt) and wait for its answer.  An executor seen
-// exited before answering (an idle exit racing the request) is relaunched: the new one
-// takes the pending request.
-void resident_call(int op, int dt, const SosxResidentDesc &d, const char *fn,
-                   const std::function<void()> &poll = {})
-{
-    Resident *R = resident_get(op, dt);
-    if (!R) raise_error("%s: resident small-path executor: HIP refused its stream or words", fn);
-    if (!R->running || __atomic_load_n(&R->ctl->exited, __ATOMIC_ACQUIRE)) resident_launch(*R, op, dt, fn);
-    R->ctl->d = d;
-    const uint64_t k = ++R->seq;
-    __atomic_store_n(&R->ctl->req, k, __ATOMIC_RELEASE);
-    const double t0 = now_s();
-    unsigned spins = 0;
-    while (__atomic_load_n(&R->ctl->done, __ATOMIC_ACQUIRE) < k) {
-        __builtin_ia32_pause();
-        if ((++spins & 0xFF) == 0 && poll) poll();
-        if ((spins & 0x3FF) != 0) continue;
-        if (__atomic_load_n(&R->ctl->exited, __ATOMIC_ACQUIRE) &&
-            __atomic_load_n(&R->ctl->done, __ATOMIC_ACQUIRE) < k)
-            resident_launch(*R, op, dt, fn);
-        if ((spins & 0xFFFFF) == 0) {
-            const hipError_t e = hipStreamQuery(R->stream);
-            if (e != hipSuccess && e != hipErrorNotReady) hip_check(e, fn);
-            if (now_s() - t0 > limit_s())
-                raise_error("%s: resident small-path executor: no answer after %.0f s", fn, limit_s());
-        }
-    }
-    g_res.calls++;
-    if (__atomic_load_n(&R->ctl->err, __ATOMIC_ACQUIRE)) {
-        __atomic_store_n(&R->ctl->err, (uint64_t)0, __ATOMIC_RELAXED);
-        raise_error("%s: small shared-memory path: timed out after %.0f s waiting for a peer's operand "
-                    "(resident executor)", fn, limit_s());
-    }
-}
-
-void resident_teardown()
-{
-    for (auto &kv : g_res.by_key) {
-        Resident &R = kv.second;
-        if (R.ctl) __atomic_store_n(&R.ctl->stop, (uint64_t)1, __ATOMIC_RELEASE);
-        if (R.stream) {
-            (void)hipStreamSynchronize(R.stream);
-            (void)hipStreamDestroy(R.stream);
-        }
-        if (R.ctl) (void)hipHostFree(R.ctl);
-    }
-    g_res.by_key.clear();
-    g_res.on = -1;
-}
-
-bool aligned16p(const void *p) { return ((uintptr_t)p & 15) == 0; }
-
 }  // namespace
 
 size_t small_shared_bytes(int npes)
@@ -396,7 +277,6 @@ void small_path_setup(void *region, size_t bytes)
 
 void small_path_teardown()
 {
-    resident_teardown();
     if (g.registered && g.host) (void)hipHostUnregister(g.host);
     if (g.out) (void)hipHostFree(g.out);
     if (g.flags) (void)hipHostFree(g.flags);
@@ -404,8 +284,6 @@ void small_path_teardown()
 }
 
 long small_path_calls() { return g.calls; }
-long small_resident_calls() { return g_res.calls; }
-long small_resident_launches() { return g_res.launches; }
 long small_path_device_calls() { return g.dev_calls; }
 
 // Collective over the world when the job is up: every PE passes the same limit (checked
@@ -623,81 +501,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         }
         g.slot_users[sl].push_back({r, k});
     }
-    // the resident executor (opt-in) takes requests up to SOSX_RESIDENT_MAX_BYTES: a device
-    // operand's staging + posts then run there too (and the fold after it, below)
-    const bool res_ok = bytes <= SOSX_RESIDENT_MAX_BYTES && resident_on();
-    const bool staged_res = staged && res_ok && nw <= 8;
-    // a recdbl_sw reduction of a device operand in ONE request: staging + posts, the waits
-    // for the peers' posts on the device, the fold
-    const bool fused = staged_res && !bcast && !sosplan::is_scan(alg) && alg != SOSX_ALG_RING && P <= 8;
-    if (staged_res) {
-        std::atomic_thread_fence(std::memory_order_seq_cst);  // the slot ids before the request
-        SosxResidentDesc d;
-        memset(&d, 0, sizeof(d));
-        d.kind = fused ? SOSX_RESIDENT_STAGE_FOLD : SOSX_RESIDENT_STAGE;
-        d.stage_src = source;
-        d.stage_dst = g.dev + slot_off(mw, sl);
-        d.stage_bytes = bytes;
-        d.stage_vec = aligned16p(source) && aligned16p(d.stage_dst) ? 1u : 0u;
-        d.nposts = (uint32_t)nw;
-        for (int k = 0; k < nw; ++k) {
-            d.post_word[k] = words[k];
-            d.post_val[k] = vals[k];
-        }
-        if (!fused) {
-            if (bcast) resident_call(SOSX_OP_BOR, SOSX_DT_UCHAR, d, fn);
-            else resident_call(op, dt, d, fn);
-        } else {
-            phase(1);
-            int from[8];
-            uint64_t want[8];
-            d.npeers = (uint32_t)P;
-            for (int i = 0; i < P; ++i) {
-                from[i] = -1;
-                if (i == me) {
-                    d.slot[i][0] = g.dev + slot_off(mw, sl);
-                    continue;
-                }
-                const int q = t.world_rank(i);
-                const uint64_t k = ++g.seen_from[q];
-                SmallCtl *qc = ctl(q);
-                d.wait_word[i] = (const uint64_t *)(g.dev + ((char *)&qc->posted[mw].v - g.host));
-                d.wait_val[i] = k;
-                d.ring_word[i] = (const uint32_t *)(g.dev + ((char *)&qc->ring[mw][k % 2] - g.host));
-                d.slot[i][0] = g.dev + slot_off(q, 0);
-                d.slot[i][1] = g.dev + slot_off(q, 1);
-                from[i] = q;
-                want[i] = k;
-            }
-            const int p2 = sosplan::pow2_floor(P), nx = P - p2;
-            const int mp = me < p2 ? me : me - p2;
-            d.np = (uint32_t)p2;
-            for (int y = 0; y < p2; ++y) {
-                const int x = y ^ mp;
-                d.leaf_idx[y] = (int8_t)x;
-                d.extra_idx[y] = (int8_t)(x < nx ? x + p2 : -1);
-            }
-            const bool direct = dev_dst || s.host_heap.contains(target, bytes);
-            d.out = direct ? target : g.out;
-            d.count = count;
-            d.vec = aligned16p(d.out) ? 1u : 0u;  // the slots are 16-B aligned
-            d.limit = (long long)(limit_s() * 1e3 * (double)g_res.khz);
-            double past[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            resident_call(op, dt, d, fn, [&]() {  // a peer that took the other path ends the job
-                for (int i = 0; i < P; ++i)
-                    if (from[i] >= 0 && ctl(from[i])->posted[mw].v.load(std::memory_order_acquire) < want[i])
-                        route_check(from[i], want[i], g.route_tag, fn, past[i]);
-            });
-            phase(3);
-            for (int i = 0; i < P; ++i)
-                if (from[i] >= 0) mine->consumed[from[i]].v.store(g.seen_from[from[i]], std::memory_order_release);
-            if (!direct) memcpy(target, g.out, bytes);
-            g.calls++;
-            g.dev_calls++;
-            trace_end();
-            return;
-        }
-    } else if (staged) {
+    if (staged) {
         std::atomic_thread_fence(std::memory_order_seq_cst);  // the slot ids before the launch
         const int rc = sosx_small_stage(g.dev + slot_off(mw, sl), source, bytes, words, vals, nw, s.stream);
         if (rc) raise_error("%s: small-path copy of a device operand failed (status %d)", fn, rc);
@@ -725,60 +529,14 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     void *out = direct ? target : g.out;  // null when this PE writes nothing
     if (++g.fseq == 0) g.fseq = 1;
     int rc = SOSX_OK, nblocks = 0;
-    // the resident executor (opt-in): recdbl_sw folds of up to 8 leaves and the linear
-    // folds (scans, broadcasts), unless a launched staging copy precedes them on the stream
-    const bool resident = res_ok && (!staged || staged_res);
-    auto run_resident = [&](int rop, int rdt, uint32_t kind, int np, const void *const *ins,
-                            const void *const *extras, size_t cnt) {
-        SosxResidentDesc d;
-        memset(&d, 0, sizeof(d));
-        d.kind = kind;
-        d.np = (uint32_t)np;
-        d.count = cnt;
-        d.out = out;
-        bool vec = aligned16p(out);
-        for (int k = 0; k < np; ++k) {
-            d.in[k] = ins[k];
-            d.extra[k] = extras ? extras[k] : nullptr;
-            vec &= aligned16p(ins[k]) && (!d.extra[k] || aligned16p(d.extra[k]));
-        }
-        d.vec = vec ? 1u : 0u;
-        resident_call(rop, rdt, d, fn);
-    };
-    if (resident && bcast) {
-        const bool copy_root = ((alg - sosplan::PLAN_BCAST) & 1) != 0;
-        if (me != root || copy_root) run_resident(SOSX_OP_BOR, SOSX_DT_UCHAR, SOSX_RESIDENT_LINEAR, 1, &in[root],
-                                                  nullptr, bytes);
-        else out = nullptr;
-    } else if (resident && sosplan::is_scan(alg) && P <= 8) {
-        const int np = alg == sosplan::PLAN_INSCAN ? me + 1 : me;
-        if (np > 0) {
-            run_resident(op, dt, SOSX_RESIDENT_LINEAR, np, in, nullptr, count);
-        } else if (dev_dst) {
-            hip_check(hipMemsetAsync(out, 0, bytes, s.stream), fn);
-            hip_check(sync_system(s.stream), fn);
-        } else {
-            memset(out, 0, bytes);
-        }
-    } else if (resident && !bcast && !sosplan::is_scan(alg) && alg != SOSX_ALG_RING &&
-               sosplan::pow2_floor(P) <= 8) {
-        const int p2 = sosplan::pow2_floor(P), nx = P - p2;
-        const int mp = me < p2 ? me : me - p2;
-        const void *leaves[8], *extras[8];
-        for (int y = 0; y < p2; ++y) {
-            const int x = y ^ mp;
-            leaves[y] = in[x];
-            extras[y] = x < nx ? in[x + p2] : nullptr;
-        }
-        run_resident(op, dt, SOSX_RESIDENT_FOLD, p2, leaves, extras, count);
-    } else if (bcast) {
+    if (bcast) {
         // 3. one launch: the root's bytes into this PE's target -- every non-root, and the
         //    root itself for the team forms (copy_root, src/collectives_c.c4:390-397); the
         //    active-set forms leave the root's target untouched (:342-378)
         const bool copy_root = ((alg - sosplan::PLAN_BCAST) & 1) != 0;
         if (me != root || copy_root)
             rc = sosx_small_linear(SOSX_OP_BOR, SOSX_DT_UCHAR, out, &in[root], 1, bytes, g.flags,
-                                   g.fseq, &nblocks, s.stream);
+                                   g.fseq, &nblocks, 1, s.stream);
         else
             out = nullptr;  // nothing written: no copy out either
     } else if (sosplan::is_scan(alg)) {
@@ -787,7 +545,7 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         //    zeros, as SOS's memset (src/collectives.c:1111-1209)
         const int np = alg == sosplan::PLAN_INSCAN ? me + 1 : me;
         if (np > 0) {
-            rc = sosx_small_linear(op, dt, out, in, np, count, g.flags, g.fseq, &nblocks, s.stream);
+            rc = sosx_small_linear(op, dt, out, in, np, count, g.flags, g.fseq, &nblocks, 1, s.stream);
         } else if (dev_dst) {
             hip_check(hipMemsetAsync(out, 0, bytes, s.stream), fn);
             hip_check(sync_system(s.stream), fn);
@@ -812,9 +570,12 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         rc = sosx_small_fold(op, dt, out, leaves, extras, p2, count, g.flags, g.fseq, &nblocks, s.stream);
     }
     if (rc) raise_error("%s: small-path reduction failed (status %d)", fn, rc);
+    // the launch read the peers' slots after their posts, each workgroup behind its own
+    // system-scope acquire (small.hip slot_acquire)
+    if (nblocks > 0) note_peer_read(true);
     // no fold launch followed the copy kernel (an active-set broadcast's root, exscan's
     // PE 0 with a host target): the call must not return while it still reads `source`
-    if (staged && !staged_res && nblocks == 0) hip_check(sync_system(s.stream), fn);
+    if (staged && nblocks == 0) hip_check(sync_system(s.stream), fn);
     phase(3);
     // 4. completion from the workgroups' flags (no stream synchronisation); then the
     //    peers' slots are read: acknowledge; my result out
@@ -874,23 +635,10 @@ bool small_local_combine(int op, int dt, void *inout, const void *in, size_t cou
     if (stage_in) memcpy(L.stage + kLocalCombineBytes, in, bytes);
     if (++L.seq == 0) L.seq = 1;
     const void *ins[2] = {io, ii};
-    if (bytes <= SOSX_RESIDENT_MAX_BYTES && resident_on()) {  // the resident executor (opt-in)
-        SosxResidentDesc d;
-        memset(&d, 0, sizeof(d));
-        d.kind = SOSX_RESIDENT_LINEAR;
-        d.np = 2;
-        d.count = count;
-        d.out = io;
-        d.in[0] = io;
-        d.in[1] = ii;
-        d.vec = aligned16p(io) && aligned16p(ii) ? 1u : 0u;
-        resident_call(op, dt, d, "shmemx_reduce_local");
-    } else {
-        int nblocks = 0;
-        const int rc = sosx_small_linear(op, dt, io, ins, 2, count, L.flags, L.seq, &nblocks, s.stream);
-        if (rc) raise_error("shmemx_reduce_local: small combine failed (status %d)", rc);
-        wait_flags(L.flags, nblocks, L.seq, "shmemx_reduce_local");
-    }
+    int nblocks = 0;
+    const int rc = sosx_small_linear(op, dt, io, ins, 2, count, L.flags, L.seq, &nblocks, 0, s.stream);
+    if (rc) raise_error("shmemx_reduce_local: small combine failed (status %d)", rc);
+    wait_flags(L.flags, nblocks, L.seq, "shmemx_reduce_local");
     if (stage_io) memcpy(inout, L.stage, bytes);
     return true;
 }
@@ -906,8 +654,6 @@ void small_local_release()
 }  // namespace sosrt
 
 extern "C" long sosx_small_path_calls(void) { return sosrt::small_path_calls(); }
-extern "C" long sosx_small_resident_calls(void) { return sosrt::small_resident_calls(); }
-extern "C" long sosx_small_resident_launches(void) { return sosrt::small_resident_launches(); }
 extern "C" long sosx_small_path_device_calls(void) { return sosrt::small_path_device_calls(); }
 extern "C" size_t sosx_set_small_device_bytes(size_t team_bytes)
 {

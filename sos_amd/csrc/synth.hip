@@ -152,18 +152,7 @@ int sosx_fill(int dtype, int dist, uint64_t seed, int pe, void *dst, size_t coun
 int sosx_memcpy(void *dst, const void *src, size_t bytes, void *stream)
 {
     static hipEvent_t ev = nullptr;
-    // diagnostic (tools/p2p_stress.py A/B): SOSX_MEMCPY_PLAIN=1 restores round 4's plain
-    // copy + hipStreamSynchronize
-    static const bool plain = [] {
-        const char *e = getenv("SOSX_MEMCPY_PLAIN");
-        return e && *e == '1';
-    }();
     hipStream_t st = as_stream(stream);
-    if (plain) {
-        hipError_t pe = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st);
-        if (pe == hipSuccess) pe = hipStreamSynchronize(st);
-        return hip_ok(pe);
-    }
     hipError_t e = ev ? hipSuccess
                       : hipEventCreateWithFlags(&ev, hipEventReleaseToSystem | hipEventDisableTiming);
     // what kernels stored before (on any stream) in HBM first, then the copy

@@ -17,6 +17,13 @@
 // Build with -DBROKEN_DRAIN to drop the drain before a round's receives are marked
 // consumed (step 4): the sanitizer must then report the race (the negative control).
 //
+// The consumer half of the memory-visibility rule is checked too:
+// the backend classifies every wait (a `posted` / `dposted` counter: a peer's bytes) and
+// every queued copy or fold (does it read another PE's heap?) on its own, and a peer read
+// with a wait since the protocol's last acquire() ends the run ("peer read without an
+// acquire").  Build with -DBROKEN_ACQUIRE to drop the acquires: the run must then fail
+// that way (the negative control).
+//
 // Stream mode runs with the entry boundary on the host, queued, and mixed across PEs.
 //
 // Usage: p2p_proto_harness [iters]     prints "p2p protocol harness: N calls OK", exit 0
@@ -97,9 +104,43 @@ constexpr size_t kHeap = 8u << 20;
     abort();
 }
 
+bool in_peer_heap(int me, const void *p)
+{
+    for (size_t q = 0; q < g_heaps.size(); ++q)
+        if ((int)q != me && (const char *)p >= g_heaps[q] && (const char *)p < g_heaps[q] + kHeap) return true;
+    return false;
+}
+
+std::atomic<long> g_acquires{0}, g_peer_reads{0};
+
 struct CpuBackend {
     Stream *s;
     bool entry_on_host;
+    int me;
+    sosp2p::Shared *sh;
+    sosp2p::AcquireTrack trk;
+    void read(bool own)
+    {
+        trk.read(own);
+        g_peer_reads++;
+        if (own) g_acquires++;
+        if (trk.unacquired) die("peer read without an acquire", me);
+    }
+    int acquire()
+    {
+#ifndef BROKEN_ACQUIRE
+        trk.acquired();
+        g_acquires++;
+        s->push([] { std::atomic_thread_fence(std::memory_order_acquire); });
+#endif
+        return 0;
+    }
+    bool data_wait(int nq, const uint64_t *const *qa)
+    {
+        for (int i = 0; i < nq; ++i)
+            if (sosp2p::in_dposted(sh, (const char *)sh, qa[i])) return true;
+        return false;
+    }
     int complete()
     {
         s->drain();
@@ -114,6 +155,9 @@ struct CpuBackend {
     }
     int gather(int n, const void *const *srcs, void *const *dsts, const size_t *bytes)
     {
+        bool peer = false;
+        for (int i = 0; i < n; ++i) peer |= in_peer_heap(me, srcs[i]);
+        if (peer) read(false);
         std::vector<const void *> sv(srcs, srcs + n);
         std::vector<void *> dv(dsts, dsts + n);
         std::vector<size_t> bv(bytes, bytes + n);
@@ -125,6 +169,11 @@ struct CpuBackend {
     int run_ops(const sosplan::Round &r, const std::vector<std::vector<const void *>> &ins,
                 const sosp2p::LocalPtr &local_ptr)
     {
+        for (const auto &in : ins) {
+            bool peer = false;
+            for (const void *p : in) peer |= in_peer_heap(me, p);
+            if (peer) read(false);
+        }
         for (size_t i = 0; i < r.ops.size(); ++i) {
             const sosplan::Local l = r.ops[i];
             const std::vector<const void *> in = ins[i];
@@ -180,6 +229,7 @@ struct CpuBackend {
     int signal(int nw, uint64_t *const *wa, const uint64_t *wv, int nq, const uint64_t *const *qa,
                const uint64_t *qv)
     {
+        if (data_wait(nq, qa)) trk.waited();
         std::vector<uint64_t *> a(wa, wa + nw);
         std::vector<uint64_t> av(wv, wv + nw);
         std::vector<const uint64_t *> q(qa, qa + nq);
@@ -191,8 +241,19 @@ struct CpuBackend {
                          uint64_t *const *wa, const uint64_t *wv, int nq, const uint64_t *const *qa,
                          const uint64_t *qv)
     {
+        // the gather's workgroups acquire after the step's waits (copy.hip k_gather<true>)
+        const bool own = data_wait(nq, qa);
         signal(nw, wa, wv, nq, qa, qv);
-        return gather(n, srcs, dsts, bytes);
+        bool peer = false;
+        for (int i = 0; i < n; ++i) peer |= in_peer_heap(me, srcs[i]);
+        if (peer) read(own);
+        std::vector<const void *> sv(srcs, srcs + n);
+        std::vector<void *> dv(dsts, dsts + n);
+        std::vector<size_t> bv(bytes, bytes + n);
+        s->push([sv, dv, bv] {
+            for (size_t i = 0; i < sv.size(); ++i) memcpy(dv[i], sv[i], bv[i]);
+        });
+        return 0;
     }
     uint64_t *dev(uint64_t *p) { return p; }
     const uint64_t *dev(const uint64_t *p) { return p; }
@@ -203,6 +264,7 @@ struct CpuBackend {
             std::this_thread::yield();
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) die(what);
         }
+        if (sosp2p::in_dposted(sh, (const char *)sh, a)) trk.waited();
     }
     void entry_hook() {}
     bool host_entry() { return entry_on_host; }
@@ -215,6 +277,7 @@ struct CpuBackend {
             std::this_thread::yield();
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) die(what);
         }
+        if (sosp2p::in_posted(sh, &a)) trk.waited();
     }
     void plan_mismatch(int pw) { die("plan mismatch", pw); }
     void phase(int) {}
@@ -244,7 +307,7 @@ void pe_main(int P, int me, int mode, const std::vector<Case> &cases, sosp2p::Sh
 {
     Stream st;
     const bool stream_mode = mode > 0;
-    CpuBackend be{&st, mode == 1 || (mode == 3 && me % 2 == 0)};
+    CpuBackend be{&st, mode == 1 || (mode == 3 && me % 2 == 0), me, sh, {}};
     sosp2p::Local loc;
     sosp2p::StreamLocal sl;
     char *heap = g_heaps[(size_t)me];
@@ -345,6 +408,9 @@ int main(int argc, char **argv)
         for (char *h : g_heaps) free(h);
     }
     free(sh);
-    printf("p2p protocol harness: %ld calls OK (host and stream signalling, both entries)\n", total);
+    if (g_peer_reads.load() == 0) die("no launch read a peer's bytes");
+    printf("p2p protocol harness: %ld calls OK (host and stream signalling, both entries); "
+           "%ld peer reads, each after an acquire (%ld acquires)\n", total, g_peer_reads.load(),
+           g_acquires.load());
     return 0;
 }

@@ -1,8 +1,11 @@
 """Readback for the multi-process GPU checkers (team_check_pe.py, coll_check_pe.py).
 
 A checker compares a PE's result with the CPU oracle's bytes ON THE CPU: the device
-result comes back through ONE D2H copy into pinned host memory (sosx_memcpy: the copy,
-then an event with a system-scope release), host results are compared where they lie.
+result comes back through ONE plain D2H copy into pinned host memory (hipMemcpy from
+libamdhip64 itself, no release or fence of the test's own in front of it: what a user's
+hipMemcpy or torch .cpu() after the call does), so the suite verifies that the library's
+own completion release (sync_system, runtime.h) put the call's stores in HBM.
+Host results are compared where they lie.
 The expected bytes are never uploaded.  Round 4's checkers uploaded the expected vector
 through a pageable torch H2D copy and counted mismatches with a kernel: a path whose
 DMA writes and kernel reads were themselves a source of stale bytes under 12-process
@@ -11,12 +14,28 @@ from a wrong result.
 
 Test infrastructure only.
 """
+import ctypes
+
 import numpy as np
 import torch
 
 from sos_amd import _lib as L
 
 _PINNED = {}
+_HIP = None
+_D2H = 2  # hipMemcpyDeviceToHost
+
+
+def _hip_memcpy():
+    """hipMemcpy of the HIP runtime libsos_amd.so runs on (dlsym through the library's
+    handle searches its dependencies: no second runtime is loaded)."""
+    global _HIP
+    if _HIP is None:
+        f = L.lib().hipMemcpy
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _HIP = f
+    return _HIP
 
 
 def device_bytes(ptr, nbytes):
@@ -28,7 +47,8 @@ def device_bytes(ptr, nbytes):
         if len(_PINNED) > 8:
             _PINNED.clear()
         t = _PINNED[nbytes] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    L.check(L.lib().sosx_memcpy(t.data_ptr(), ptr, nbytes, None), "sosx_memcpy")
+    rc = _hip_memcpy()(t.data_ptr(), ptr, nbytes, _D2H)
+    assert rc == 0, f"hipMemcpy D2H failed ({rc})"
     return t.numpy().copy()
 
 

@@ -90,10 +90,6 @@ def main():
     if bad:
         print(f"PE {me}/{P}: {len(bad)} of {checks} checks FAILED: {bad[:6]}", flush=True)
         return 1
-    lib = L.lib() if hasattr(L, "lib") else None
-    if lib is not None and os.environ.get("SHMEMX_SMALL_RESIDENT") == "1":
-        print(f"PE {me}/{P}: resident calls {lib.sosx_small_resident_calls()} "
-              f"launches {lib.sosx_small_resident_launches()}", flush=True)
     print(f"PE {me}/{P}: {checks} checks OK (small-path calls {small}, device {small_dev})", flush=True)
     return 0
 

@@ -451,7 +451,7 @@ def test_small_linear_kernel(torch_cuda, np_, dt, op, layout):
         nb = ctypes.c_int(-1)
         rc = L.sosx_small_linear(op, dt, ctypes.c_void_p(optr), (ctypes.c_void_p * np_)(*ptr), np_,
                                  ctypes.c_size_t(n), ctypes.c_void_p(flags.data_ptr()),
-                                 ctypes.c_uint32(seq), ctypes.byref(nb), None)
+                                 ctypes.c_uint32(seq), ctypes.byref(nb), seq % 2, None)
         assert rc == 0
         torch.cuda.synchronize()
         assert 1 <= nb.value <= (n + 255) // 256

@@ -236,20 +236,6 @@ def test_reduce_local_small(torch_cuda, shmem1, oracle, dt, op):
         finally:
             S.lib().shmem_free(hb)
             S.lib().shmem_free(ha)
-    if os.environ.get("SHMEMX_SMALL_RESIDENT") == "1":  # test_reduce_local_small_resident
-        assert S.lib().sosx_small_resident_calls() > 0
-
-
-def test_reduce_local_small_resident():
-    """The same calls with SHMEMX_SMALL_RESIDENT=1 (a fresh process): combines of at most
-    4 KiB on the resident executor, the rest on launches, every result the oracle's; then
-    with a 50 us idle limit, so the executor exits between calls and is relaunched."""
-    here = os.path.abspath(__file__)
-    for idle in ("2000", "50"):
-        r = _run([sys.executable, "-m", "pytest", here, "-q", "-p", "no:cacheprovider", "-k",
-                  "test_reduce_local_small and not resident"], timeout=300,
-                 env={"SHMEMX_SMALL_RESIDENT": "1", "SHMEMX_SMALL_RESIDENT_IDLE_US": idle})
-        assert r.returncode == 0 and "6 passed" in r.stdout, (idle, r.stdout[-2000:], r.stderr[-2000:])
 
 
 def _run(cmd, timeout=120, env=None):

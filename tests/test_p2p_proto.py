@@ -9,6 +9,11 @@ PE, in and out of place, misaligned operands, each result checked.  Built with
 the peer's writes, and every overwrite after the peers' reads, by the protocol's
 counters alone.  The negative control drops the drain before a
 round's receives are marked consumed and must be reported.
+
+The same runs check the consumer half of the memory-visibility rule:
+the backend classifies waits and launches itself, and every launch that reads a peer's
+bytes must follow an acquire issued after the wait for the peer's post.  The negative
+control drops the protocol's acquires and must be caught.
 """
 import os
 import subprocess
@@ -42,6 +47,7 @@ def test_host_protocol_race_free(harness):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
     assert "calls OK" in r.stdout and int(r.stdout.split(":")[1].split()[0]) > 8000, r.stdout
+    assert "peer reads, each after an acquire" in r.stdout, r.stdout
 
 
 def test_broken_protocol_is_caught():
@@ -50,3 +56,10 @@ def test_broken_protocol_is_caught():
     r = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode != 0
     assert "ThreadSanitizer: data race" in r.stderr or "wrong result" in r.stderr, r.stderr[-3000:]
+
+
+def test_missing_acquire_is_caught():
+    exe = _build("p2p_proto_harness_noacq", "-DBROKEN_ACQUIRE")
+    r = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=900)
+    assert r.returncode != 0
+    assert "peer read without an acquire" in r.stderr, r.stderr[-3000:]
