@@ -315,11 +315,38 @@ def host_resident(args, torch):
         out[f"{kind}_pipelined_GiBs"] = round(n * es / t / GiB, 3)
         out[f"{kind}_pipelined_ms"] = round(t * 1e3, 3)
         del ha, hb
+    out["static_data"] = static_data_row(args)
     out["bytes_moved_per_call"] = {"H2D": 2 * n * es, "D2H": n * es}
     out["note"] = ("payload GiB/s of reduce_local on host-resident operands through the GPU: "
                    "H2D(inout, in) + combine + D2H(inout); serial vs 3-stream chunk pipeline "
-                   "(sosx_combine_host); PCIe Gen5 x16 = 63 GB/s per direction (spec)")
+                   "(sosx_combine_host); static_data: the same pipeline on two static arrays of "
+                   "an SOS-style C program (examples/static_reduce.c), whose data segment "
+                   "shmem_init registers with HIP as SOS registers it (src/init.c:341-346); "
+                   "PCIe Gen5 x16 = 63 GB/s per direction (spec)")
     return out
+
+
+def static_data_row(args):
+    """shmemx_reduce_local on STATIC symmetric arrays: examples/static_reduce (a C program,
+    fp32 sum only, at most 128Mi elements) run as a child process on the same GPU."""
+    exe = os.path.join(HERE, "examples", "static_reduce")
+    if args.dtype != "float" or args.op != "sum" or args.n > (128 << 20):
+        return {"skipped": "examples/static_reduce covers fp32 sum up to 128Mi elements"}
+    if not os.path.exists(exe):
+        return {"skipped": "examples/static_reduce not built (make -C examples)"}
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+              "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    try:
+        r = subprocess.run([exe, "local", str(args.n), "5"], capture_output=True, text=True,
+                           timeout=300, env=env)
+        row = json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001  (reported in the line, never fatal for the bench)
+        return {"error": f"{type(e).__name__}: {e}"}
+    if r.returncode != 0 or row.get("wrong"):
+        row["error"] = f"exit {r.returncode}: {r.stderr[-300:]}"
+    return row
 
 
 def multi_stream_setup(args, torch, kind):

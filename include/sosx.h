@@ -256,6 +256,12 @@ void sosx_acquire_stats(long *acquires, long *peer_reads, long *unacquired, unsi
  * rewritten) and OR-ing its XCD id into *xcc_mask (device memory, or null). */
 int sosx_acquire_system(unsigned *xcc_mask, void *stream);
 
+/* The executable's data segment [__data_start, _end) as shmem_init registered it with
+ * HIP (SOS registers it with every transport, src/init.c:341-346): its page-rounded base
+ * in *base (may be null) and its size; 0 when it is not registered
+ * (SHMEMX_REGISTER_DATA=0, or HIP refused the range). */
+size_t sosx_data_segment(void **base);
+
 /* The p2p transport's mapping flags (introspection for tests): the hipHostRegister
  * flags of the shared pair-counter segment and the hipIpcOpenMemHandle flags of a peer's
  * device heap. */

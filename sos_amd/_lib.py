@@ -99,6 +99,7 @@ _SIGS = {
     "sosx_rccl_comm_count": (_c.c_int, []),
     "sosx_release_workspaces": (_c.c_size_t, []),
     "sosx_sys_releases": (_c.c_long, []),
+    "sosx_data_segment": (_c.c_size_t, [_c.POINTER(_c.c_void_p)]),
     "sosx_acquire_stats": (None, [_c.POINTER(_c.c_long), _c.POINTER(_c.c_long), _c.POINTER(_c.c_long),
                                   _c.POINTER(_c.c_uint)]),
     "sosx_acquire_system": (_c.c_int, [_c.c_void_p, _c.c_void_p]),

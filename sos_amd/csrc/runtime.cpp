@@ -200,6 +200,8 @@ static const EnvDef kEnv[] = {
      "Largest operand of that path (its slots: at most 32 MiB over all PEs)"},
     {"SHMEMX_SMALL_DEVICE", "size", "131072", "device",
      "Device-resident operands take that path when team size * bytes <= this (0: never)"},
+    {"SHMEMX_REGISTER_DATA", "bool", "true", "device",
+     "Register the executable's data segment with HIP (static symmetric objects DMA as pinned)"},
 };
 
 static void print_env()
@@ -259,6 +261,50 @@ static void read_env(State &s)
     s.rccl_allreduce = ar ? std::min(std::max(atoi(ar), 0), 2) : 0;
     s.sym_stage_bytes = (s.sym_stage_bytes + 4095) & ~(size_t)4095;
     if (s.sym_stage_bytes >= s.dev_heap_bytes) s.dev_heap_bytes = s.sym_stage_bytes + (256u << 20);
+    const char *rd = getenv("SHMEMX_REGISTER_DATA");
+    s.register_data = !(rd && (!strcmp(rd, "0") || !strcasecmp(rd, "false") || !strcasecmp(rd, "no")));
+}
+
+// ---------------------------------------------------------------------------------
+// The executable's data segment.  SOS registers it with every transport at init
+// (src/init.c:341-346 takes [__data_start, _end); src/transport_ofi.c:741 fi_mr_reg of
+// shmem_internal_data_base, src/transport_xpmem.c:56-64), so static symmetric objects
+// move like heap memory.  Here the same range is registered with HIP: its pages are
+// pinned and mapped for the DMA engines, so H2D/D2H copies of static operands run at the
+// pinned rate instead of through HIP's pageable bounce buffers (sosx_combine_host's chunk
+// pipeline and the team path's staging copies detect it as host-registered memory).  The
+// range is rounded out to whole pages; if HIP refuses it (a read-only page at the start),
+// the start is rounded in instead; if that fails too the segment stays pageable: correct,
+// slower, reported under SHMEM_DEBUG.  Unregistered at shmem_finalize.
+// ---------------------------------------------------------------------------------
+static void register_data_segment(State &s)
+{
+    s.data_reg = nullptr;
+    s.data_reg_bytes = 0;
+    if (!s.register_data || !__data_start || !_end || _end <= __data_start) return;
+    const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+    const uintptr_t lo = (uintptr_t)__data_start, hi = ((uintptr_t)_end + pg - 1) & ~(pg - 1);
+    for (uintptr_t start : {lo & ~(pg - 1), (lo + pg - 1) & ~(pg - 1)}) {
+        if (start >= hi) break;
+        const hipError_t e = hipHostRegister((void *)start, hi - start, hipHostRegisterDefault);
+        if (e == hipSuccess) {
+            s.data_reg = (void *)start;
+            s.data_reg_bytes = hi - start;
+            debug_msg("data segment [%p, %p) registered with HIP (%zu B)", (void *)start, (void *)hi,
+                      (size_t)(hi - start));
+            return;
+        }
+        (void)hipGetLastError();
+        debug_msg("hipHostRegister of the data segment from %p failed (%s)", (void *)start,
+                  hipGetErrorString(e));
+    }
+}
+
+static void unregister_data_segment(State &s)
+{
+    if (s.data_reg) (void)hipHostUnregister(s.data_reg);
+    s.data_reg = nullptr;
+    s.data_reg_bytes = 0;
 }
 
 // ---------------------------------------------------------------------------------
@@ -685,6 +731,7 @@ static void init_common(int pe, int npes, const ncclUniqueId *uid)
     s.team_pool.assign((size_t)s.teams_max, nullptr);
     s.initialized = true;
     s.finalized = false;
+    register_data_segment(s);
     if (s.want_p2p || s.ext_base) ensure_device_heap();
     if (s.shm.extra && npes > 1)
         small_path_setup((char *)s.shm.extra + shm_p2p_region_bytes(), small_shared_bytes(npes));
@@ -837,6 +884,7 @@ void shmem_finalize(void)
         }
     if (s.sys_ev) (void)hipEventDestroy(s.sys_ev);
     s.sys_ev = nullptr;
+    unregister_data_segment(s);
     if (s.acq_mask) (void)hipFree(s.acq_mask);
     s.acq_mask = nullptr;
     for (hipStream_t *ps : {&s.pipe_h2d, &s.pipe_d2h}) {
@@ -1070,6 +1118,14 @@ int sosx_rccl_comm_count(void)
 // How many system-scope completion markers (sync_system / release_system) this PE has
 // issued: every call that returns data ends with one (introspection for tests).
 long sosx_sys_releases(void) { return st().sys_releases; }
+
+// The executable's data segment as registered with HIP at shmem_init (null / 0: not
+// registered: SHMEMX_REGISTER_DATA=0, or HIP refused it).
+size_t sosx_data_segment(void **base)
+{
+    if (base) *base = st().data_reg;
+    return st().data_reg_bytes;
+}
 
 void sosx_acquire_stats(long *acquires, long *peer_reads, long *unacquired, unsigned *xcc_mask)
 {

@@ -126,6 +126,9 @@ struct State {
     bool debug = false;
     bool error_checking = true;
     bool heap_on_device = false;
+    bool register_data = true;        // SHMEMX_REGISTER_DATA: register the data segment
+    void *data_reg = nullptr;         // the registered page range of [__data_start, _end)
+    size_t data_reg_bytes = 0;
     // teams (src/shmem_team.c): predefined WORLD / SHARED / SHMEMX_TEAM_NODE occupy slots
     // 0..2 of SHMEM_TEAMS_MAX; team_avail has a bit per free slot
     Team world, shared, node;

@@ -6,13 +6,18 @@ plans' transfers become direct reads of peer HBM, synchronised through node shar
 memory -- the same code that reads xGMI peer memory on the 8-GPU node.  (RCCL refuses
 two ranks on one GPU; tests/test_gpu_fakerccl.py runs the RCCL executor's multi-PE cases.)
 """
+import json
 import os
 import re
 import subprocess
 import sys
 import time
 
+import numpy as np
 import pytest
+
+from oracle import oracle as O
+from sos_amd import _lib as L
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -280,6 +285,54 @@ def test_peer_reads_follow_system_acquire(np_):
         r.stdout + r.stderr[-2000:]
     assert all(int(reads) > 0 and int(acq) > 0 for _, _, reads, acq, _ in ok), ok
     assert {m for *_, m in ok} == {"ff"}, ok
+
+
+def _static_inputs(n, pe):
+    i = np.arange(n, dtype=np.uint64)
+    k = (i * np.uint64(2654435761) + np.uint64(pe * 40503)) % np.uint64(1000003)
+    return k.astype(np.float32) * np.float32(0.001)
+
+
+@pytest.mark.parametrize("np_", [1, 2])
+def test_static_data_team_reduce(examples, np_, tmp_path):
+    """shmem_float_sum_reduce on STATIC source/dest arrays of 16Mi floats (.bss of
+    examples/static_reduce.c), which shmem_init registered with HIP as SOS registers its
+    data segment (src/init.c:341-346): every PE's bytes equal the oracle's (the ring under
+    AUTO; one PE copies), and the segment was registered."""
+    n = 16 << 20
+    out = str(tmp_path / "static")
+    cmd = [os.path.join(examples, "static_reduce"), "team", str(n), out]
+    if np_ == 1:
+        env = dict(os.environ)
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            env.pop(k, None)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env)
+    else:
+        r = oshrun(np_, cmd, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    reg = re.findall(r"PE (\d+)/\d+: static team reduce of \d+ floats written; data segment "
+                     r"registered (\d+) B", r.stdout)
+    assert sorted(int(p) for p, _ in reg) == list(range(np_)), r.stdout
+    assert all(int(b) >= 2 * n * 4 for _, b in reg), reg
+    ins = [_static_inputs(n, q) for q in range(np_)]
+    dt = L.dtype_id("float")
+    exp = O.ring(L.op_id("sum"), dt, ins) if np_ > 1 else [ins[0]]
+    for q in range(np_):
+        got = np.fromfile(f"{out}.{q}", dtype=np.float32)
+        assert got.size == n and got.tobytes() == exp[q].tobytes(), q
+
+
+def test_static_data_local_combine(examples):
+    """shmemx_reduce_local on static arrays (the H2D || combine || D2H pipeline) on the
+    registered data segment: exact results."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([os.path.join(examples, "static_reduce"), "local", str(16 << 20), "3"],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["wrong"] == 0 and res["registered_bytes"] >= 2 * (16 << 20) * 4, res
 
 
 def test_small_device_setter_is_collective():
