@@ -374,6 +374,20 @@ def test_team_management(np_):
     assert r.returncode == 0 and sorted(map(int, ok)) == list(range(np_)), r.stdout + r.stderr[-3000:]
 
 
+def _fracs_above_one(obj, path=""):
+    """Every key named frac* whose value is a number above 1, with its path."""
+    out = []
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            if k.startswith("frac") and isinstance(v, (int, float)) and v > 1:
+                out.append((path + "/" + k, v))
+            out += _fracs_above_one(v, path + "/" + k)
+    elif isinstance(obj, list):
+        for i, v in enumerate(obj):
+            out += _fracs_above_one(v, f"{path}[{i}]")
+    return out
+
+
 @pytest.mark.parametrize("np_", [2, 4])
 def test_bench_team_leg(np_):
     """The driver's N > 1 bench path (torch.distributed.run -> bench.py -> team_bench) with
@@ -405,6 +419,10 @@ def test_bench_team_leg(np_):
     assert res["config"]["gpus_used"] == 1 and res["config"]["parallelism"] == f"pe{np_}_on_1gpu"
     assert f"{np_} PEs on 1 GPU (shared" in res["config"]["workload"], res["config"]
     assert res["check"]["bitwise_mismatches_all_ranks"] == 0
+    # no xGMI link carried these bytes: no link roofline, and no fraction above 1 anywhere
+    assert res["team_roofline"]["bound"] == "shared-gpu", res["team_roofline"]
+    assert res["team_roofline"]["frac_one_link"] is None, res["team_roofline"]
+    assert _fracs_above_one(res) == [], _fracs_above_one(res)
     # both p2p signalling modes measured and checked in every leg
     assert list(res["transports"]) == ["p2p", "p2p_host"], res["transports"]
     for t in ("p2p", "p2p_host"):

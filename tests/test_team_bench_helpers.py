@@ -196,3 +196,18 @@ def test_headline_fields_n2():
     assert "1->8 scaling curve plots this" in f["value_definition"]
     none = TB.headline_fields(2, 8, 4, None, [-1, -1])
     assert none["value"] is None and none["algbw_GiBs"] is None and none["rccl_comm_ranks"] == [-1, -1]
+
+
+def test_xgmi_fractions_null_when_ranks_share_a_gpu():
+    """N = 2 ranks on one device: no xGMI link carries the bytes, so the line carries no
+    link roofline (bound "shared-gpu", fractions null) however fast the step was -- round
+    5's line printed frac_one_link 7.4 there.  With one GPU per rank the fractions are
+    the link rates' (and a real step cannot exceed 7 links)."""
+    wire = 2 * (2 - 1) / 2 * (128 << 20) * 4
+    fast = 1e-5  # far faster than any link: only a shared device can do that
+    f = TB.xgmi_fields(wire, fast, world=2, ngpus=1)
+    assert f["frac_one_link"] is None and f["frac_7_links"] is None and f["busbw_GBs"] > 0
+    assert TB.team_bound(2, 1) == "shared-gpu" and TB.team_bound(8, 8) == "xgmi"
+    g = TB.xgmi_fields(wire, 0.01, world=2, ngpus=2)
+    assert abs(g["frac_one_link"] - wire / 0.01 / 1e9 / TB.XGMI_LINK_GBS) < 1e-3
+    assert 0 < g["frac_7_links"] < g["frac_one_link"] <= 1

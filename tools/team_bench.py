@@ -83,6 +83,22 @@ def headline_fields(world, n, es, t_step, rccl_ranks):
             "rccl_comm_ranks": list(rccl_ranks)}
 
 
+def xgmi_fields(wire, ts, world, ngpus):
+    """busbw = wire bytes per PE / step time, and its fractions of one and of seven xGMI
+    links.  When ranks share a GPU no xGMI link carries their bytes, so the link roofline
+    does not describe the run: the fractions are null (a fraction above 1 would say the
+    roofline is wrong, not that the code beat it) and the bound is "shared-gpu"."""
+    bus = wire / ts / 1e9
+    shared = ngpus < world
+    return {"busbw_GBs": round(bus, 1),
+            "frac_one_link": None if shared else round(bus / XGMI_LINK_GBS, 3),
+            "frac_7_links": None if shared else round(bus / (XGMI_LINK_GBS * XGMI_LINKS), 3)}
+
+
+def team_bound(world, ngpus):
+    return "shared-gpu" if ngpus < world else "xgmi"
+
+
 def select_primary(results):
     """(transport `value` comes from, None) or (None, reason).  Only a VALUE_T transport
     that was measured and whose bitwise check is clean on every rank qualifies; there is
@@ -288,7 +304,7 @@ def main(args, torch, pmc=None):
             results[tname]["tolerance_violations"] = int(mmt[1].item())
 
     curve = size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
-                       src, dst, stream, sorted(sweep_sizes + [n]), results) if sweep_sizes else {}
+                       src, dst, stream, sorted(sweep_sizes + [n]), results, ngpus) if sweep_sizes else {}
 
     schedules = {} if getattr(args, "no_adjacent", False) else \
         other_schedules(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world,
@@ -343,9 +359,7 @@ def main(args, torch, pmc=None):
         return {"ms_per_step": round(ts * 1e3, 4),
                 "value_GiBs": round(world * n * es / ts / GiB, 3),
                 "algbw_GiBs": round(n * es / ts / GiB, 3),
-                "busbw_GBs": round(wire / ts / 1e9, 1),
-                "frac_one_link": round(wire / ts / 1e9 / XGMI_LINK_GBS, 3),
-                "frac_7_links": round(wire / ts / 1e9 / (XGMI_LINK_GBS * XGMI_LINKS), 3),
+                **xgmi_fields(wire, ts, world, ngpus),
                 "xfer_ms_per_step": round(rr["prof"]["xfer_ms"] / max(rr["prof"]["ncall"], 1), 4),
                 "fold_ms_per_step": round(rr["prof"]["fold_ms"] / max(rr["prof"]["ncall"], 1), 4),
                 "bitwise_mismatches_all_ranks": rr["mismatches"],
@@ -385,7 +399,8 @@ def main(args, torch, pmc=None):
                      **({"note": "p2p: the fold reads its P-1 peer inputs in place over xGMI, "
                                  "so this launch is link-bound (see team_roofline)"}
                         if primary and primary.startswith("p2p") else {})},
-        "team_roofline": dict(bound="xgmi", wire_bytes_per_pe=int(wire), **team_roof(r)) if r else None,
+        "team_roofline": dict(bound=team_bound(world, ngpus), wire_bytes_per_pe=int(wire),
+                              **team_roof(r)) if r else None,
         "check": {"bitwise_mismatches_all_ranks": r["mismatches"] if r else None,
                   "against": "on-GPU regeneration of all PE inputs + schedule-order fold"},
     }
@@ -768,7 +783,7 @@ def host_resident_team(args, torch, dist, L, S, fn, team, dt, es, dist_kind, see
 
 
 def size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank, world, src, dst,
-               stream, sizes, headline):
+               stream, sizes, headline, ngpus):
     """The team reduction over nreduce = 1Mi .. 256Mi (SURVEY 8(d) config #5 / the north
     star's 1->8-GPU curve) on each transport: whole-job GiB/s (world * n * s / t, max over
     ranks), busbw = 2(P-1)/P * n * s / t and its fraction of one xGMI link and of all 7.
@@ -800,9 +815,7 @@ def size_curve(args, torch, dist, L, S, fn, team, dt, es, dist_kind, seed, rank,
             wire = 2 * (P - 1) / P * m * es
             row = {"nreduce": m, "ms_per_call": round(ts * 1e3, 4),
                    "value_GiBs": round(world * m * es / ts / GiB, 3),
-                   "busbw_GBs": round(wire / ts / 1e9, 1),
-                   "frac_one_link": round(wire / ts / 1e9 / XGMI_LINK_GBS, 3),
-                   "frac_7_links": round(wire / ts / 1e9 / (XGMI_LINK_GBS * XGMI_LINKS), 3)}
+                   **xgmi_fields(wire, ts, world, ngpus)}
             if m == sizes[-1] and m != args.n:
                 cseed = seed + 211 + tid
                 L.fill(dt, dist_kind, cseed, rank, src, m, 0, stream)
