@@ -74,6 +74,8 @@ def fold(args):
     out = {}
     for name, offs in (("congruent", [0] * P), ("input0+4", [4] + [0] * (P - 1)), ("all+4", [4] * P), ("all+8", [8] * P), ("all+12", [12] * P),
                         ("mixed", [(4 * (k + 1)) % 16 for k in range(P)])):
+        if args.only and name not in args.only.split(","):
+            continue
         ins = [base[k] + offs[k] for k in range(P)]
         for k in range(P):
             L.fill(23, 0, 0x5EED, k, ins[k], n, 0, st)
@@ -112,6 +114,8 @@ def prefix(args):
     out = {}
     for name, offs in (("congruent", [0] * P), ("input0+4", [4] + [0] * (P - 1)), ("all+4", [4] * P),
                        ("mixed", [(4 * (k + 1)) % 16 for k in range(P)])):
+        if args.only and name not in args.only.split(","):
+            continue
         ins = [base[k] + offs[k] for k in range(P)]
         for k in range(P):
             L.fill(23, 0, 0x5EED, k, ins[k], n, 0, st)
@@ -136,6 +140,7 @@ if __name__ == "__main__" and "--prefix" in sys.argv:
     sys.argv.remove("--prefix")
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated layouts (default: all)")
     prefix(ap.parse_args())
     sys.exit(0)
 
@@ -144,6 +149,7 @@ if __name__ == "__main__" and "--fold" in sys.argv:
     sys.argv.remove("--fold")
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated layouts (default: all)")
     fold(ap.parse_args())
     sys.exit(0)
 
