@@ -349,6 +349,65 @@ __global__ __launch_bounds__(kThreads) void k_prefix_buf(PrefixPtrs p, Geom g)
     }
 }
 
+// Realigning 8-input fold variants (round 6): the product's
+// k_fold_realign_np loads two aligned vectors per incongruent input and reached 1.30x the
+// algorithmic read bytes in FETCH_SIZE with 6 of 8 inputs incongruent
+// (profiles/r6_realign_pmc.txt).  MODE 1: the second vector by a plain load (may hit the
+// line the first load brought into L2); MODE 2: both loads plain; MODE 3: the second
+// vector from the next lane by DPP wave_shl:1 (lane 63 loads it); MODE 4: the same through
+// __shfl_down.  Same element order as k_fold_realign_np.
+template <class T, class OP, int NP, int ORDER, int MODE>
+__global__ __launch_bounds__(kThreads) void k_fold_realign_v(T *out, FoldRealignArgs a, Geom g)
+{
+    const size_t nblk = gridDim.x;
+    const bool last_lane = (threadIdx.x & 63) == 63;
+    u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
+    const u32x4 *I[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+        I[k] = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>((const T *)a.p[k] + g.head) - a.d[k]);
+    for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
+        const size_t i = t * (size_t)kThreads + threadIdx.x;
+        u32x4 x[NP], y[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) x[k] = ldv<MODE != 2>(I[k] + i);
+        if constexpr (MODE <= 2) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                if (a.d[k]) y[k] = ldv<MODE == 0>(I[k] + i + 1);
+        } else {
+            if (last_lane) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k)
+                    if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
+            }
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                if (a.d[k]) {
+                    u32x4 nx;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        if constexpr (MODE == 3)
+                            nx[c] = (unsigned)__builtin_amdgcn_update_dpp((int)0, (int)x[k][c], 0x130, 0xf, 0xf, false);
+                        else
+                            nx[c] = __shfl_down(x[k][c], 1u);
+                    }
+                    if (!last_lane) y[k] = nx;
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            if (a.d[k]) x[k] = realign16(x[k], y[k], a.d[k]);
+        stv<true>(O + i, fold_pack<T, OP, NP, ORDER>(x));
+    }
+    if (g.has_rem && blockIdx.x == nblk - 1) {
+        constexpr int V = Pack<T>::N;
+        for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = fold_runtime_np_elem<T, OP, ORDER>(a, i);
+        for (size_t i = g.head + g.tiles * (size_t)(kThreads * V) + threadIdx.x; i < g.n; i += kThreads)
+            out[i] = fold_runtime_np_elem<T, OP, ORDER>(a, i);
+    }
+}
+
 }  // namespace sos
 
 using namespace sos;
@@ -802,6 +861,32 @@ int sosxv_ping_launch(void *ctl, long long idle_ticks, int nap, void *stream)
     return hip_ok(hipGetLastError());
 }
 
+
+// The 8-input LINEAR fp32-sum fold with inputs at other 16-B offsets, realign shape
+// `mode` (k_fold_realign_v; 0 = the product's k_fold_realign_np loads).
+int sosxv_fold_realign(int mode, void *out, const void *const *ins, size_t n, void *stream)
+{
+    Geom g = make_geom((uintptr_t)out, n, sizeof(float), 1);
+    FoldRealignArgs a;
+    memset(&a, 0, sizeof(a));
+    a.np = 8;
+    for (int k = 0; k < 8; ++k) {
+        a.p[k] = ins[k];
+        a.d[k] = (unsigned)((uintptr_t)((const float *)ins[k] + g.head) & 15);
+        if ((uintptr_t)ins[k] % sizeof(float)) return SOSX_ERR_ARG;
+    }
+    const hipStream_t st = as_stream(stream);
+    const dim3 grid(grid_for(g, kNoCap)), blk(kThreads);
+    switch (mode) {
+        case 0: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 0>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 1: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 1>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 2: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 2>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 3: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 3>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 4: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 4>), grid, blk, 0, st, (float *)out, a, g); break;
+        default: return SOSX_ERR_ARG;
+    }
+    return hip_ok(hipGetLastError());
+}
 
 int sosxv_num_combine(void) { return kNumCombine; }
 const char *sosxv_combine_name(int v) { return v >= 0 && v < kNumCombine ? kCombineNames[v] : ""; }
