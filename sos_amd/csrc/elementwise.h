@@ -246,6 +246,16 @@ __device__ __forceinline__ u32x4 realign16(const u32x4 &lo, const u32x4 &hi, uns
     return v;
 }
 
+// The 16-B vector of the next lane of the wave (lane l gets lane l + 1's; lane 63 gets
+// zeros and must supply its own): four DPP wave_shl:1 moves, no LDS and no memory access.
+__device__ __forceinline__ u32x4 next_lane16(const u32x4 &x)
+{
+    u32x4 v;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)x[c], 0x130, 0xf, 0xf, false);
+    return v;
+}
+
 constexpr int kThreads = 256;
 
 // Geometry of one (out, a, b) or fold call, computed on the host:

@@ -142,13 +142,21 @@ __device__ __forceinline__ T fold_runtime_np_elem(const FoldRealignArgs &a, size
     }
 }
 
-// Inputs at different offsets: every input's aligned vector is loaded first, then the
-// second vector of each incongruent input, then the fold.
+// Inputs at different offsets: every input's aligned vector is loaded once; an
+// incongruent input's second vector -- the next lane's first -- comes from that lane by
+// DPP (next_lane16), and only the wave's last lane loads its own.  Round 5 loaded the
+// second vector in every lane: with nontemporal loads L2 did not keep the line for the
+// second request, so reads reached 1.30x the algorithmic bytes with 6 of 8 inputs
+// incongruent (profiles/r6_realign_pmc.txt).  Over 1..8 incongruent inputs of 8 x 16Mi
+// fp32 (tools/realign_ab.py, profiles/r6_realign_ab.txt) this shape is the fastest or
+// within 1 % up to 6 (m = 1 6.21, m = 3 6.10, m = 6 5.64 TB/s against 6.22 / 5.68 / 5.05
+// for round 5's) and 2 % behind plain double loads at 8.
 template <class T, class OP, int NP, int ORDER>
 __global__ __launch_bounds__(kThreads) void k_fold_realign_np(T *out, FoldRealignArgs a, Geom g)
 {
     constexpr int V = Pack<T>::N;
     const size_t nblk = gridDim.x;
+    const bool last_lane = (threadIdx.x & 63) == 63;
     u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
     const u32x4 *I[NP];
 #pragma unroll
@@ -159,12 +167,18 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_np(T *out, FoldRealig
         u32x4 x[NP], y[NP];
 #pragma unroll
         for (int k = 0; k < NP; ++k) x[k] = ldv<true>(I[k] + i);
+        if (last_lane) {  // its next vector belongs to the next wave (or workgroup)
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
+        }
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
-#pragma unroll
-        for (int k = 0; k < NP; ++k)
-            if (a.d[k]) x[k] = realign16(x[k], y[k], a.d[k]);
+            if (a.d[k]) {
+                const u32x4 nx = next_lane16(x[k]);
+                if (!last_lane) y[k] = nx;
+                x[k] = realign16(x[k], y[k], a.d[k]);
+            }
         stv<true>(O + i, fold_pack<T, OP, NP, ORDER>(x));
     }
     if (g.has_rem && blockIdx.x == nblk - 1) {
@@ -306,15 +320,19 @@ struct PrefixRealignArgs {
     int np;
 };
 
-// P known at compile time (round 5, as k_fold_realign_np): every input's aligned vector,
-// then the second vector of each incongruent input, then the prefix.  Replaced a
-// runtime-P kernel that branched per input between its loads (profiles/r5_fold_outshift.txt:
-// 8 x 16Mi fp32, input 0 at +4 B 4.06 -> 5.79-5.82 TB/s, every input at +4 3.39 -> 4.57).
+// P known at compile time (round 5, as k_fold_realign_np; it replaced a runtime-P kernel
+// that branched per input between its loads, profiles/r5_fold_outshift.txt): every
+// input's aligned vector (the wave's last lane also loads its incongruent inputs' next
+// vectors), the other lanes' next vectors by DPP from the neighbouring lane (round 6, as
+// k_fold_realign_np: round 5's second load per lane read 1.42x the algorithmic bytes,
+// profiles/r6_realign_pmc.txt), then the prefix.  Every load of the tile still precedes
+// the first store (aliasing, as k_prefix).
 template <class T, class OP, int NP>
 __global__ __launch_bounds__(kThreads) void k_prefix_realign_np(PrefixRealignArgs a, Geom g)
 {
     constexpr int V = Pack<T>::N;
     const size_t nblk = gridDim.x;
+    const bool last_lane = (threadIdx.x & 63) == 63;
     const u32x4 *I[NP];
     u32x4 *O[NP];
 #pragma unroll
@@ -327,12 +345,18 @@ __global__ __launch_bounds__(kThreads) void k_prefix_realign_np(PrefixRealignArg
         u32x4 x[NP], y[NP];
 #pragma unroll
         for (int k = 0; k < NP; ++k) x[k] = ldv<true>(I[k] + i);
+        if (last_lane) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
+        }
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
-#pragma unroll
-        for (int k = 0; k < NP; ++k)
-            if (a.d[k]) x[k] = realign16(x[k], y[k], a.d[k]);
+            if (a.d[k]) {
+                const u32x4 nx = next_lane16(x[k]);
+                if (!last_lane) y[k] = nx;
+                x[k] = realign16(x[k], y[k], a.d[k]);
+            }
         u32x4 acc = x[0];
         stv<true>(O[0] + i, acc);
 #pragma unroll

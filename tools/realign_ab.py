@@ -15,8 +15,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-NAMES = {0: "two nt loads (product)", 1: "nt + plain second load", 2: "two plain loads",
-         3: "nt + DPP wave_shl:1", 4: "nt + __shfl_down"}
+NAMES = {0: "two nt loads (round 5)", 1: "nt + plain second load", 2: "two plain loads",
+         3: "nt + DPP wave_shl:1", 4: "nt + __shfl_down", 5: "plain incongruent, 2 loads",
+         6: "plain + DPP", 7: "plain incongruent + DPP"}
 
 
 def main():
@@ -41,7 +42,10 @@ def main():
     base = [((b.data_ptr() + 4095) & ~4095) + 4096 * (k % 8) for k, b in enumerate(bufs)]
     out, ref = base[P], base[P + 1]
     modes = [int(m) for m in args.only.split(",")] if args.only else sorted(NAMES)
-    layouts = {"mixed": [(4 * (k + 1)) % 16 for k in range(P)], "all+4": [4] * P}
+    layouts = {"mixed": [(4 * (k + 1)) % 16 for k in range(P)], "all+4": [4] * P,
+               "input0+4": [4] + [0] * (P - 1), "two+4": [4, 0, 0, 0, 4, 0, 0, 0]}
+    for m in range(1, P + 1):  # m<k>: inputs 0..k-1 at 4, 8, 12, 4, ... bytes, the rest congruent
+        layouts[f"m{m}"] = [4 * (j % 3 + 1) if j < m else 0 for j in range(P)]
     res = {}
     for lay in args.layouts.split(","):
         offs = layouts[lay]

@@ -355,7 +355,9 @@ __global__ __launch_bounds__(kThreads) void k_prefix_buf(PrefixPtrs p, Geom g)
 // (profiles/r6_realign_pmc.txt).  MODE 1: the second vector by a plain load (may hit the
 // line the first load brought into L2); MODE 2: both loads plain; MODE 3: the second
 // vector from the next lane by DPP wave_shl:1 (lane 63 loads it); MODE 4: the same through
-// __shfl_down.  Same element order as k_fold_realign_np.
+// __shfl_down; MODE 5: two loads, plain for the incongruent inputs and nt for the
+// congruent ones; MODE 6: plain loads + DPP; MODE 7: MODE 5's policy + DPP.  Same element
+// order as k_fold_realign_np.
 template <class T, class OP, int NP, int ORDER, int MODE>
 __global__ __launch_bounds__(kThreads) void k_fold_realign_v(T *out, FoldRealignArgs a, Geom g)
 {
@@ -369,9 +371,14 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_v(T *out, FoldRealign
     for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
         const size_t i = t * (size_t)kThreads + threadIdx.x;
         u32x4 x[NP], y[NP];
+        constexpr bool kSplit = MODE == 5 || MODE == 7;  // nt only for congruent inputs
+        constexpr bool kNt = MODE == 0 || MODE == 1 || MODE == 3 || MODE == 4;
 #pragma unroll
-        for (int k = 0; k < NP; ++k) x[k] = ldv<MODE != 2>(I[k] + i);
-        if constexpr (MODE <= 2) {
+        for (int k = 0; k < NP; ++k) {
+            if constexpr (kSplit) x[k] = a.d[k] ? ldv<false>(I[k] + i) : ldv<true>(I[k] + i);
+            else x[k] = ldv<kNt>(I[k] + i);
+        }
+        if constexpr (MODE <= 2 || MODE == 5) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 if (a.d[k]) y[k] = ldv<MODE == 0>(I[k] + i + 1);
@@ -379,7 +386,7 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_v(T *out, FoldRealign
             if (last_lane) {
 #pragma unroll
                 for (int k = 0; k < NP; ++k)
-                    if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
+                    if (a.d[k]) y[k] = ldv<kNt>(I[k] + i + 1);
             }
 #pragma unroll
             for (int k = 0; k < NP; ++k)
@@ -387,7 +394,7 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_v(T *out, FoldRealign
                     u32x4 nx;
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-                        if constexpr (MODE == 3)
+                        if constexpr (MODE != 4)
                             nx[c] = (unsigned)__builtin_amdgcn_update_dpp((int)0, (int)x[k][c], 0x130, 0xf, 0xf, false);
                         else
                             nx[c] = __shfl_down(x[k][c], 1u);
@@ -883,6 +890,9 @@ int sosxv_fold_realign(int mode, void *out, const void *const *ins, size_t n, vo
         case 2: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 2>), grid, blk, 0, st, (float *)out, a, g); break;
         case 3: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 3>), grid, blk, 0, st, (float *)out, a, g); break;
         case 4: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 4>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 5: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 5>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 6: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 6>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 7: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 7>), grid, blk, 0, st, (float *)out, a, g); break;
         default: return SOSX_ERR_ARG;
     }
     return hip_ok(hipGetLastError());
