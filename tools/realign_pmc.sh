@@ -7,7 +7,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-out=gpurun_out/realign_pmc
+out=gpurun_out/realign_pmc${REALIGN_TAG:-}
 mkdir -p "$out"
 R=$(pwd)
 run() {  # name seconds cmd...
