@@ -151,13 +151,31 @@ __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g, Sig<kMaxGate>
                 const uint64_t j = j0 + (uint64_t)u * kThreads;
                 if (j < nv) v[u] = __builtin_nontemporal_load(src + j);
             }
-        } else {  // src at another 16-B offset: two aligned vectors, funnel-shifted
+        } else {  // src at another 16-B offset: aligned vectors j and j + 1, funnel-shifted
+            // vector j + 1 is the next lane's vector j: taken by DPP (next_lane16), loaded
+            // only by the wave's last lane -- a second nt load in every lane re-fetched the
+            // lines (the fold's case, profiles/r6_realign_pmc.txt).  Lanes load vector j up
+            // to j == nv: the straddled vector after the body holds bytes of the segment.
+            const bool last_lane = (threadIdx.x & 63) == 63;
+            u32x4 lo[kGatherU], hi[kGatherU];
 #pragma unroll
             for (int u = 0; u < kGatherU; ++u) {
                 const uint64_t j = j0 + (uint64_t)u * kThreads;
-                if (j < nv)
-                    v[u] = realign16(__builtin_nontemporal_load(src + j),
-                                     __builtin_nontemporal_load(src + j + 1), sd);
+                if (j <= nv) lo[u] = __builtin_nontemporal_load(src + j);
+            }
+            if (last_lane) {
+#pragma unroll
+                for (int u = 0; u < kGatherU; ++u) {
+                    const uint64_t j = j0 + (uint64_t)u * kThreads;
+                    if (j < nv) hi[u] = __builtin_nontemporal_load(src + j + 1);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kGatherU; ++u) {
+                const uint64_t j = j0 + (uint64_t)u * kThreads;
+                const u32x4 nx = next_lane16(lo[u]);
+                if (!last_lane) hi[u] = nx;
+                if (j < nv) v[u] = realign16(lo[u], hi[u], sd);
             }
         }
 #pragma unroll
