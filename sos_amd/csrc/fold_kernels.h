@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_np(T *out, FoldRealig
 // one another: the p2p ring's in-place fold of the peers' sources when source and target
 // sit at different offsets in the symmetric heap).  Fold in the inputs' frame, one vector
 // per input per lane, and realign the OUTPUT: out vector i = realign16(F_i, F_i+1, d),
-// F_i+1 taken from the next lane; the last lane of each wave folds its F_i+1 itself
+// F_i+1 taken from the next lane (DPP); the last lane of each wave folds its F_i+1 itself
 // (k_fold_realign_np would load two vectors per input: 4.2-4.4 TB/s here, 5.8-6.1 this way).
 template <class T, class OP, int NP, int ORDER>
 __global__ __launch_bounds__(kThreads) void k_fold_outshift(T *out, FoldRealignArgs a, Geom g)
@@ -216,9 +216,7 @@ __global__ __launch_bounds__(kThreads) void k_fold_outshift(T *out, FoldRealignA
             for (int k = 0; k < NP; ++k) y[k] = ldv<true>(I[k] + i + 1);
         }
         const u32x4 f = fold_pack<T, OP, NP, ORDER>(x);
-        u32x4 nx;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) nx[c] = __shfl_down(f[c], 1u);
+        u32x4 nx = next_lane16(f);  // DPP (round 6; __shfl_down was an LDS bpermute)
         if (last_lane) nx = fold_pack<T, OP, NP, ORDER>(y);
         stv<true>(O + i, realign16(f, nx, d));
     }
@@ -386,7 +384,7 @@ __global__ __launch_bounds__(kThreads) void k_prefix_realign_np(PrefixRealignArg
 
 // Every input at the SAME 16-B offset d != 0 from the (congruent) outputs: the prefix in
 // the inputs' frame, each output realigned (k_fold_outshift's scheme, once per output:
-// the next lane's running value by __shfl_down, the last lane of a wave folding the next
+// the next lane's running value by DPP (next_lane16), the last lane of a wave folding the next
 // vector itself).  Aliasing as k_prefix: every load of the tile before the first store.
 template <class T, class OP, int NP>
 __global__ __launch_bounds__(kThreads) void k_prefix_outshift(PrefixRealignArgs a, Geom g)
@@ -418,9 +416,7 @@ __global__ __launch_bounds__(kThreads) void k_prefix_outshift(PrefixRealignArgs 
                 acc = apply<T, OP>(acc, x[k]);
                 if (last_lane) accn = apply<T, OP>(accn, y[k]);
             }
-            u32x4 nx;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) nx[c] = __shfl_down(acc[c], 1u);
+            u32x4 nx = next_lane16(acc);
             if (last_lane) nx = accn;
             stv<true>(O[k] + i, realign16(acc, nx, d));
         }
