@@ -222,14 +222,19 @@ int launch_step(const Sig<kMaxGate> &gate, hipStream_t st)
     return hip_ok(hipGetLastError());
 }
 
-// Copy nseg (src, dst, bytes) segments, <= 16 per launch.  (A gate rides in the launch
-// when it has at most kGateMaxBlocks tiles.)  `gate` (or null): a signalling
-// step that must precede the copies -- carried by the first launch when its grid is
-// small enough, else run by its own k_p2p_signal launch first.
+// Copy nseg (src, dst, bytes) segments, <= 16 per launch.  `gate` (or null): a
+// signalling step that must precede the copies.  It rides in the copy launch when the
+// whole gather is ONE launch of at most kGateMaxBlocks tiles (each workgroup acquires
+// after its own wait); otherwise it runs as its own k_p2p_signal launch, followed -- when
+// it awaits posts -- by the acquire kernel, so every copy launch reads the peers' bytes
+// behind a system-scope acquire.
 int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,
                 const Sig<kMaxGate> *gate, hipStream_t st)
 {
     bool gate_pending = gate != nullptr;
+    int live = 0;
+    for (int i = 0; i < nseg; ++i) live += bytes[i] != 0;
+    const bool one_launch = live <= kMaxSeg;
     for (int base = 0; base < nseg; base += kMaxSeg) {
         GatherArgs g;
         memset(&g, 0, sizeof(g));
@@ -260,12 +265,13 @@ int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size
         if (blocks > 0xffffffffull) return SOSX_ERR_ARG;
         Sig<kMaxGate> none;
         memset(&none, 0, sizeof(none));
-        if (gate_pending && blocks <= kGateMaxBlocks) {
+        if (gate_pending && one_launch && blocks <= kGateMaxBlocks) {
             hipLaunchKernelGGL(k_gather<true>, dim3((unsigned)blocks), dim3(kThreads), 0, st, g, *gate);
             gate_pending = false;
         } else {
-            if (gate_pending) {  // large grid: the step as its own launch
+            if (gate_pending) {  // large or several grids: the step as its own launch
                 if (launch_step(*gate, st) != SOSX_OK) return SOSX_ERR_HIP;
+                if (gate->nq > 0 && sosx_acquire_system(nullptr, st) != SOSX_OK) return SOSX_ERR_HIP;
                 gate_pending = false;
             }
             hipLaunchKernelGGL(k_gather<false>, dim3((unsigned)blocks), dim3(kThreads), 0, st, g, none);
