@@ -8,8 +8,9 @@ library classifies its waits and launches itself and counts (sosx_acquire_stats)
 acquires issued, peer reads, and peer reads with a wait since the last acquire.  This
 checks, deterministically and per call, that every team call read peers' bytes, issued
 acquires, and left the unacquired count at 0 -- reductions under four schedules in both
-p2p signalling modes, a scan, a broadcast, and the small path with host and device
-operands -- and that every result is the oracle's, read back by a plain D2H copy
+p2p signalling modes at 1Mi + 3 elements and under two at 16Ki + 3 (gathers small enough
+to carry their signalling step), a scan, a broadcast, and the small path with host and
+device operands -- and that every result is the oracle's, read back by a plain D2H copy
 (tests/readback.py).  Prints one line per PE with the XCD mask of the acquire kernels.
 
 Test infrastructure: the oracle is the checker only.
@@ -83,6 +84,19 @@ def main():
              O.scan(op, dt, ins, False)[me], dget, reads=me != 0)
         call(f"broadcast signal {mode}", lambda: S.shmem_float_broadcast(world, ddst, dsrc, n, 0),
              ins[0], dget, reads=me != 0)
+    # mid-size device operands (past SHMEMX_SMALL_DEVICE, gathers of <= 256 KiB): in stream
+    # mode the signalling step rides in the gather launch, which acquires per workgroup
+    mid = 16384 + 3
+    mins = [O.fill(dt, 0, 93, q, mid) for q in range(P)]
+    L.check(L.lib().sosx_memcpy(dsrc, mins[me].ctypes.data, mid * 4, None), "sosx_memcpy")
+    for mode in modes:
+        for alg in ("auto", "recdbl_gather"):
+            S.shmemx_set_reduce_algorithm(L.ALGS[alg])
+            res = S.lib().sosx_resolve_alg(L.ALGS[alg], mid * 4, 16384)
+            exp = (O.ring(op, dt, mins) if res == L.ALGS["ring"] else O.recdbl(op, dt, mins))[me]
+            call(f"mid {alg} signal {mode}", lambda: S.shmem_float_sum_reduce(world, ddst, dsrc, mid), exp,
+                 lambda: R.device_bytes(ddst, mid * 4))
+    S.shmemx_set_reduce_algorithm(L.ALGS["auto"])
     # the small path: host-heap operands, then small device-heap operands
     m = 64
     sins = [O.fill(dt, 0, 92, q, m) for q in range(P)]

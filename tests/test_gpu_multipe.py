@@ -270,7 +270,7 @@ def test_calls_end_with_system_release(np_):
         r.stdout + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("np_", [2, 3])
+@pytest.mark.parametrize("np_", [2, 3, 4])
 def test_peer_reads_follow_system_acquire(np_):
     """The consumer half of the visibility rule: every launch that
     read a peer's bytes -- p2p gathers and in-place folds under four schedules in both
