@@ -322,17 +322,24 @@ def test_static_data_team_reduce(examples, np_, tmp_path):
         assert got.size == n and got.tobytes() == exp[q].tobytes(), q
 
 
-def test_static_data_local_combine(examples):
+@pytest.mark.parametrize("register", [True, False])
+def test_static_data_local_combine(examples, register):
     """shmemx_reduce_local on static arrays (the H2D || combine || D2H pipeline) on the
-    registered data segment: exact results."""
+    registered data segment, and with SHMEMX_REGISTER_DATA=0 (pageable): exact results."""
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
+    if not register:
+        env["SHMEMX_REGISTER_DATA"] = "0"
     r = subprocess.run([os.path.join(examples, "static_reduce"), "local", str(16 << 20), "3"],
                        capture_output=True, text=True, timeout=180, env=env)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
-    assert res["wrong"] == 0 and res["registered_bytes"] >= 2 * (16 << 20) * 4, res
+    assert res["wrong"] == 0, res
+    if register:
+        assert res["registered_bytes"] >= 2 * (16 << 20) * 4, res
+    else:
+        assert res["registered_bytes"] == 0, res
 
 
 def test_small_device_setter_is_collective():
