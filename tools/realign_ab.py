@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 
 NAMES = {0: "two nt loads (round 5)", 1: "nt + plain second load", 2: "two plain loads",
          3: "nt + DPP wave_shl:1", 4: "nt + __shfl_down", 5: "plain incongruent, 2 loads",
-         6: "plain + DPP", 7: "plain incongruent + DPP"}
+         6: "plain + DPP", 7: "plain incongruent + DPP", 8: "DPP + LDS across waves"}
 
 
 def main():

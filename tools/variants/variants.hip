@@ -372,7 +372,7 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_v(T *out, FoldRealign
         const size_t i = t * (size_t)kThreads + threadIdx.x;
         u32x4 x[NP], y[NP];
         constexpr bool kSplit = MODE == 5 || MODE == 7;  // nt only for congruent inputs
-        constexpr bool kNt = MODE == 0 || MODE == 1 || MODE == 3 || MODE == 4;
+        constexpr bool kNt = MODE == 0 || MODE == 1 || MODE == 3 || MODE == 4 || MODE == 8;
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
             if constexpr (kSplit) x[k] = a.d[k] ? ldv<false>(I[k] + i) : ldv<true>(I[k] + i);
@@ -382,6 +382,35 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_v(T *out, FoldRealign
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 if (a.d[k]) y[k] = ldv<MODE == 0>(I[k] + i + 1);
+        } else if constexpr (MODE == 8) {
+            // DPP within the wave; across waves the next wave's lane 0 vector through LDS,
+            // so only the workgroup's last lane loads (one extra vector per tile, not four)
+            __shared__ u32x4 first[kThreads / 64][NP];
+            const unsigned wave = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k)
+                    if (a.d[k]) first[wave][k] = x[k];
+            }
+            const bool wg_last = threadIdx.x == kThreads - 1;
+            if (wg_last) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k)
+                    if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
+            }
+            __syncthreads();
+            if (last_lane && !wg_last) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k)
+                    if (a.d[k]) y[k] = first[wave + 1][k];
+            }
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                if (a.d[k]) {
+                    const u32x4 nx = next_lane16(x[k]);
+                    if (!last_lane) y[k] = nx;
+                }
+            __syncthreads();  // first[] is rewritten by the next tile
         } else {
             if (last_lane) {
 #pragma unroll
@@ -893,6 +922,7 @@ int sosxv_fold_realign(int mode, void *out, const void *const *ins, size_t n, vo
         case 5: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 5>), grid, blk, 0, st, (float *)out, a, g); break;
         case 6: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 6>), grid, blk, 0, st, (float *)out, a, g); break;
         case 7: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 7>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 8: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 8>), grid, blk, 0, st, (float *)out, a, g); break;
         default: return SOSX_ERR_ARG;
     }
     return hip_ok(hipGetLastError());
