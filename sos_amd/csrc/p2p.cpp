@@ -397,7 +397,18 @@ struct HipBackend {
     int complete() { return sosrt::complete(stream) == hipSuccess ? 0 : 1; }
     int drain() { return hipStreamSynchronize(stream) == hipSuccess ? 0 : 1; }
     int release() { return release_system(stream) == hipSuccess ? 0 : 1; }
-    int acquire() { return acquire_system(stream) == hipSuccess ? 0 : 1; }
+    int acquire()
+    {
+#ifdef SOSX_TEST_HOOKS
+        // A/B of the acquire's price (test build only, tools/acquire_cost.sh): skip it
+        static const bool skip = [] {
+            const char *e = getenv("SOSX_TEST_NO_ACQUIRE");
+            return e && *e == '1';
+        }();
+        if (skip) return 0;
+#endif
+        return acquire_system(stream) == hipSuccess ? 0 : 1;
+    }
     bool device_data_wait(int nq, const uint64_t *const *qa)
     {
         for (int i = 0; i < nq; ++i)

@@ -270,21 +270,48 @@ int main(int argc, char **argv)
                    ms / K, 2.0 * sbytes / (ms / K * 1e-3) / 1e12);
         }
     }
-    // the acquire kernel as an extra launch: small kernel chains with and without it
+    // the acquire as an extra step: small kernel chains with nothing, the acquire kernel,
+    // a default-flag event record (HIP: system-scope acquire + release fence), or an event
+    // without the system fence, before each kernel; GPU time (events) and host wall time
+    hipEvent_t ev_nofence;
+    CK(hipEventCreateWithFlags(&ev_nofence, hipEventDisableSystemFence | hipEventDisableTiming));
+    const char *steps[] = {"nothing", "acquire kernel", "default event record", "event without system fence"};
     for (int rep = 0; rep < 3; ++rep) {
-        for (int acq = 0; acq < 2; ++acq) {
+        for (int acq = 0; acq < 4; ++acq) {
             const int K = 200;
             CK(hipStreamSynchronize(s));
+            auto w0 = std::chrono::steady_clock::now();
             CK(hipEventRecord(e0, s));
             for (int k = 0; k < K; ++k) {
-                if (acq) hipLaunchKernelGGL(k_acquire, dim3(64), dim3(64), 0, s, mask);
+                if (acq == 1) hipLaunchKernelGGL(k_acquire, dim3(64), dim3(64), 0, s, mask);
+                if (acq == 2) CK(hipEventRecord(ev_default, s));
+                if (acq == 3) CK(hipEventRecord(ev_nofence, s));
                 hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
             }
             CK(hipEventRecord(e1, s));
             CK(hipEventSynchronize(e1));
+            auto w1 = std::chrono::steady_clock::now();
             float ms;
             CK(hipEventElapsedTime(&ms, e0, e1));
-            printf("empty-kernel chain, acquire kernel before each=%d: %.2f us per step\n", acq, ms * 1e3 / K);
+            printf("empty-kernel chain, before each: %-28s %.2f us per step (host wall %.2f us)\n", steps[acq],
+                   ms * 1e3 / K, std::chrono::duration<double, std::micro>(w1 - w0).count() / K);
+        }
+    }
+    // one call's worth from an idle stream: host waits, then [acquire] + kernel + sync
+    for (int rep = 0; rep < 2; ++rep) {
+        for (int acq = 0; acq < 3; ++acq) {
+            const int K = 200;
+            double tot = 0;
+            for (int k = 0; k < K; ++k) {
+                CK(hipStreamSynchronize(s));
+                auto w0 = std::chrono::steady_clock::now();
+                if (acq == 1) hipLaunchKernelGGL(k_acquire, dim3(64), dim3(64), 0, s, mask);
+                if (acq == 2) CK(hipEventRecord(ev_default, s));
+                hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
+                CK(hipStreamSynchronize(s));
+                tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count();
+            }
+            printf("idle stream, launch + sync, before the kernel: %-22s %.2f us host wall\n", steps[acq], tot / K);
         }
     }
     printf("done\n");
