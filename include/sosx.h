@@ -251,6 +251,10 @@ long sosx_sys_releases(void);
  * tests. */
 void sosx_acquire_stats(long *acquires, long *peer_reads, long *unacquired, unsigned *xcc_mask);
 
+/* Of those acquires, the stream-wide acquire kernels the p2p transport enqueued (the rest
+ * ran in the workgroups of the small consuming launches themselves).  For tests. */
+long sosx_acquire_kernels(void);
+
 /* One acquire kernel on `stream`: 64 workgroups, each running a system-scope acquire
  * (buffer_inv sc0 sc1: this CU's L1 and its XCD's L2 drop lines other agents may have
  * rewritten) and OR-ing its XCD id into *xcc_mask (device memory, or null). */

@@ -102,6 +102,7 @@ _SIGS = {
     "sosx_data_segment": (_c.c_size_t, [_c.POINTER(_c.c_void_p)]),
     "sosx_acquire_stats": (None, [_c.POINTER(_c.c_long), _c.POINTER(_c.c_long), _c.POINTER(_c.c_long),
                                   _c.POINTER(_c.c_uint)]),
+    "sosx_acquire_kernels": (_c.c_long, []),
     "sosx_acquire_system": (_c.c_int, [_c.c_void_p, _c.c_void_p]),
     "sosx_gather": (_c.c_int, [_c.c_int, _c.POINTER(_c.c_void_p), _c.POINTER(_c.c_void_p),
                                _c.POINTER(_c.c_size_t), _c.c_void_p]),

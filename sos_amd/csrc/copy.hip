@@ -70,25 +70,19 @@ __global__ __launch_bounds__(kMaxSig) void k_p2p_signal(SigArgs a) { sig_step(a,
 // bytes are read after a wait that saw its post; this GPU's L2s may still hold lines of
 // the same addresses from an earlier call, and a kernel dispatch does not promise to drop
 // them (tools/acquire_probe.hip: a kernel queued behind a device-side wait read a whole
-// rewritten buffer stale).  A system-scope acquire does: buffer_inv sc0 sc1 drops this
-// CU's L1 and the non-local lines of its XCD's L2.  Its cost rules out one per workgroup of
-// a streaming kernel (a 1 GiB copy 6.6 -> 1.1 TB/s, profiles/r6_acquire_probe.txt), so
-// the transport enqueues THIS kernel once per consuming step instead (+2.1 us): 64
-// one-wave workgroups, dealt round-robin over the 8 XCDs, each fencing and recording its
-// XCD id (the mask tests read).  The next launch on the stream starts after it completes.
+// rewritten buffer stale).  A system-scope acquire does (elementwise.h wg_acquire).  Small
+// consuming grids carry it in each workgroup (carry_acquire below); a streaming grid
+// cannot (a 1 GiB copy 6.6 -> 1.1 TB/s, profiles/r6_acquire_probe.txt), so THIS kernel
+// runs once before it: 64 one-wave workgroups, dealt round-robin over the 8 XCDs, each
+// fencing and recording its XCD id (the mask tests read).  The next launch on the stream
+// starts after it completes.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void acquire_system_wg()
-{
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: buffer_inv sc0 sc1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 constexpr unsigned kAcquireBlocks = 64;
 
 __global__ __launch_bounds__(64) void k_acquire_system(unsigned *xcc_mask)
 {
     if (threadIdx.x == 0) {
-        acquire_system_wg();
+        acquire_system_lane();
         if (xcc_mask) {
             unsigned id;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(id));
@@ -106,6 +100,7 @@ struct GatherArgs {
     uint64_t bytes[kMaxSeg];
     uint64_t tstart[kMaxSeg + 1];  // prefix sums of each segment's tiles
     int nseg;
+    int acquire;               // each workgroup acquires before its loads (carry_acquire)
 };
 
 // A gather whose launch also carries the preceding p2p signalling step: every workgroup
@@ -126,15 +121,14 @@ constexpr uint64_t kTileVec = (uint64_t)kThreads * kGatherU;
 template <bool GATED>
 __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g, Sig<kMaxGate> gate)
 {
+    bool acq = g.acquire != 0;
     if constexpr (GATED) {
         sig_step(gate, threadIdx.x);
         // the awaited posts published peers' bytes: this workgroup's own acquire before
         // its loads (at most kGateMaxBlocks workgroups, so the price is one invalidate each)
-        if (gate.nq > 0) {
-            if (threadIdx.x == 0) acquire_system_wg();
-            __syncthreads();
-        }
+        acq |= gate.nq > 0;
     }
+    if (acq) wg_acquire();
     const uint64_t t = blockIdx.x;
     if (t < g.tstart[g.nseg]) {
         int s = 0;
@@ -225,12 +219,21 @@ int launch_step(const Sig<kMaxGate> &gate, hipStream_t st)
 // Copy nseg (src, dst, bytes) segments, <= 16 per launch.  `gate` (or null): a
 // signalling step that must precede the copies.  It rides in the copy launch when the
 // whole gather is ONE launch of at most kGateMaxBlocks tiles (each workgroup acquires
-// after its own wait); otherwise it runs as its own k_p2p_signal launch, followed -- when
-// it awaits posts -- by the acquire kernel, so every copy launch reads the peers' bytes
-// behind a system-scope acquire.
+// after its own wait); otherwise it runs as its own k_p2p_signal launch and -- when it
+// awaits posts -- the copies owe the acquire (carry_acquire: in their workgroups, or the
+// acquire kernel first), so every copy launch reads the peers' bytes behind a
+// system-scope acquire.  The copies' sources are peer memory
+// whenever the transport asked for an acquire.
 int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size_t *bytes,
                 const Sig<kMaxGate> *gate, hipStream_t st)
 {
+    AcquireCarry &c = acquire_carry();
+    const bool peer_was = c.peer;
+    struct Restore {
+        AcquireCarry &c;
+        bool peer;
+        ~Restore() { c.peer = peer; }
+    } restore{c, peer_was};
     bool gate_pending = gate != nullptr;
     int live = 0;
     for (int i = 0; i < nseg; ++i) live += bytes[i] != 0;
@@ -266,14 +269,22 @@ int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size
         Sig<kMaxGate> none;
         memset(&none, 0, sizeof(none));
         if (gate_pending && one_launch && blocks <= kGateMaxBlocks) {
+            g.acquire = carry_acquire(st, (unsigned)blocks);
+            if (g.acquire < 0) return SOSX_ERR_HIP;
             hipLaunchKernelGGL(k_gather<true>, dim3((unsigned)blocks), dim3(kThreads), 0, st, g, *gate);
+            if (gate->nq > 0 && !g.acquire) ++c.carried;  // acquired after the step's own wait
             gate_pending = false;
         } else {
             if (gate_pending) {  // large or several grids: the step as its own launch
                 if (launch_step(*gate, st) != SOSX_OK) return SOSX_ERR_HIP;
-                if (gate->nq > 0 && sosx_acquire_system(nullptr, st) != SOSX_OK) return SOSX_ERR_HIP;
+                if (gate->nq > 0) {  // it awaited posts: the copies owe the acquire
+                    c.want = true;
+                    c.peer = true;
+                }
                 gate_pending = false;
             }
+            g.acquire = carry_acquire(st, (unsigned)blocks);
+            if (g.acquire < 0) return SOSX_ERR_HIP;
             hipLaunchKernelGGL(k_gather<false>, dim3((unsigned)blocks), dim3(kThreads), 0, st, g, none);
         }
         if (hipGetLastError() != hipSuccess) return SOSX_ERR_HIP;
@@ -283,6 +294,29 @@ int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size
 }
 
 }  // namespace
+
+namespace sos {
+
+AcquireCarry &acquire_carry()
+{
+    static thread_local AcquireCarry c;
+    return c;
+}
+
+int carry_acquire(hipStream_t st, unsigned grid, bool can)
+{
+    AcquireCarry &c = acquire_carry();
+    if (!c.want || !c.peer) return 0;
+    if (can && grid <= kCarryMaxGrid) {
+        ++c.carried;
+        return 1;
+    }
+    c.want = false;
+    const int rc = c.stream_wide ? c.stream_wide(st) : sosx_acquire_system(nullptr, st);
+    return rc == 0 ? 0 : -1;
+}
+
+}  // namespace sos
 
 extern "C" {
 

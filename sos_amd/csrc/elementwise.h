@@ -16,6 +16,7 @@
 #include <string.h>
 #include <type_traits>
 
+#include "carry.h"
 #include "dtypes.h"
 #include "ldbl.h"
 #include "sosx.h"
@@ -262,12 +263,37 @@ constexpr int kThreads = 256;
 //   elements [0, head)                  scalar, by the remainder workgroup
 //   vectors  [0, tiles * kThreads * U)  16-B packets from element `head`
 //   elements [head + tiles*kThreads*U*V, n) scalar, by the remainder workgroup
+//   acquire: the launch carries the transport's consumer-side acquire (wg_acquire)
 struct Geom {
     size_t n;
     size_t head;
     size_t tiles;
     int has_rem;
+    int acquire;
 };
+
+// ---------------------------------------------------------------------------------
+// The consumer half of the memory-visibility rule: a launch that
+// reads bytes a peer published after a wait must not read lines this GPU's L2s kept from
+// an earlier call.  A system-scope acquire (buffer_inv sc0 sc1) drops this CU's L1 and
+// the non-local lines of its XCD's L2.  wg_acquire: lane 0 of the workgroup fences and
+// waits for the invalidate; the workgroup's loads follow the barrier.  Small grids carry
+// it this way (one invalidate per workgroup, no extra launch); streaming grids take the
+// acquire kernel first (copy.hip k_acquire_system), since one invalidate per workgroup
+// of a streaming grid costs 6x (profiles/r6_acquire_probe.txt).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void acquire_system_lane()
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: buffer_inv sc0 sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void wg_acquire()
+{
+    if (threadIdx.x == 0) acquire_system_lane();
+    __syncthreads();
+}
+
 
 
 constexpr size_t kNoCap = (size_t)1 << 31;  // hardware grid x-dimension limit
@@ -289,6 +315,7 @@ inline Geom make_geom(uintptr_t addr0, size_t n, size_t s, int U)
     const size_t nvec = (n - head) / V;
     g.tiles = nvec / (size_t)(kThreads * U);
     g.has_rem = (head > 0) || (g.tiles * (size_t)(kThreads * U) * V != n - head);
+    g.acquire = 0;
     return g;
 }
 

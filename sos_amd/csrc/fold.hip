@@ -44,8 +44,9 @@ __device__ __forceinline__ void prefix_elem_dyn(const PrefixPtrs &p, int np, int
 
 // Runtime P (any P <= 64, or 16-B incongruent operands): element loads.
 template <class T, class OP>
-__global__ __launch_bounds__(kThreads) void k_prefix_dyn(PrefixPtrs p, int np, int own, size_t n)
+__global__ __launch_bounds__(kThreads) void k_prefix_dyn(PrefixPtrs p, int np, int own, size_t n, int acquire)
 {
+    if (acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
     const size_t stride = (size_t)gridDim.x * kThreads;
     for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
         prefix_elem_dyn<T, OP>(p, np, own, i);
@@ -73,6 +74,8 @@ template <class T, class OP, int NP>
 int launch_prefix_np(const PrefixPtrs &p, size_t n, hipStream_t st)
 {
     Geom g = make_geom((uintptr_t)p.out[0], n, sizeof(T), kPrefixU);
+    g.acquire = carry_acquire(st, grid_for(g, kNoCap));
+    if (g.acquire < 0) return SOSX_ERR_HIP;
     hipLaunchKernelGGL((k_prefix<T, OP, NP, kPrefixU, true>), dim3(grid_for(g, kNoCap)),
                        dim3(kThreads), occupancy_lds(2 * NP), st, p, g);
     return hip_ok(hipGetLastError());
@@ -108,6 +111,8 @@ struct PrefixFn {
                     bool same = true;
                     for (int k = 0; k < np; ++k) same &= a.d[k] == a.d[0];
                     const bool outshift = same && a.d[0] != 0 && prefix_outshift_on();
+                    g.acquire = carry_acquire(st, grid_for(g, kNoCap));
+                    if (g.acquire < 0) return SOSX_ERR_HIP;
                     switch (np) {
 #define SOSX_PREFIX_RA(P)                                                                                  \
     case P:                                                                                                \
@@ -141,8 +146,10 @@ struct PrefixFn {
         }
         size_t blocks = (n + kThreads - 1) / kThreads;
         if (blocks > 8192) blocks = 8192;
+        const int acq = carry_acquire(st, (unsigned)blocks);
+        if (acq < 0) return SOSX_ERR_HIP;
         hipLaunchKernelGGL((k_prefix_dyn<T, OP>), dim3((unsigned)blocks), dim3(kThreads), 0, st, *p,
-                           np, own, n);
+                           np, own, n, acq);
         return hip_ok(hipGetLastError());
     }
 };
@@ -185,6 +192,7 @@ int sosx_fold(int op, int dtype, int order, void *out, const void *const *ins, i
     const size_t bytes = count * sos_dtype_info(dtype).size;
     if (nin == 1) {
         if (out == ins[0]) return SOSX_OK;
+        if (carry_acquire(as_stream(stream), 0, false) < 0) return SOSX_ERR_HIP;  // a library copy
         return hip_ok(hipMemcpyAsync(out, ins[0], bytes, hipMemcpyDeviceToDevice, as_stream(stream)));
     }
     FoldPtrs fp;

@@ -65,6 +65,7 @@ __device__ __forceinline__ u32x4 fold_pack(const u32x4 (&x)[NP])
 template <class T, class OP, int NP, int ORDER, int U>
 __global__ __launch_bounds__(kThreads) void k_fold(T *out, FoldPtrs ins, Geom g)
 {
+    if (g.acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
     constexpr int V = Pack<T>::N;
     u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
     for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
@@ -154,6 +155,7 @@ __device__ __forceinline__ T fold_runtime_np_elem(const FoldRealignArgs &a, size
 template <class T, class OP, int NP, int ORDER>
 __global__ __launch_bounds__(kThreads) void k_fold_realign_np(T *out, FoldRealignArgs a, Geom g)
 {
+    if (g.acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
     constexpr int V = Pack<T>::N;
     const size_t nblk = gridDim.x;
     const bool last_lane = (threadIdx.x & 63) == 63;
@@ -197,6 +199,7 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_np(T *out, FoldRealig
 template <class T, class OP, int NP, int ORDER>
 __global__ __launch_bounds__(kThreads) void k_fold_outshift(T *out, FoldRealignArgs a, Geom g)
 {
+    if (g.acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
     constexpr int V = Pack<T>::N;
     const size_t nblk = gridDim.x;
     const unsigned d = a.d[0];
@@ -265,6 +268,7 @@ constexpr int kPrefixU = 1;
 template <class T, class OP, int NP, int U, bool NT = true>
 __global__ __launch_bounds__(kThreads) void k_prefix(PrefixPtrs p, Geom g)
 {
+    if (g.acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
     constexpr int V = Pack<T>::N;
     for (size_t t = blockIdx.x; t < g.tiles; t += gridDim.x) {
         const size_t base = t * (size_t)(kThreads * U) + threadIdx.x;
@@ -328,6 +332,7 @@ struct PrefixRealignArgs {
 template <class T, class OP, int NP>
 __global__ __launch_bounds__(kThreads) void k_prefix_realign_np(PrefixRealignArgs a, Geom g)
 {
+    if (g.acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
     constexpr int V = Pack<T>::N;
     const size_t nblk = gridDim.x;
     const bool last_lane = (threadIdx.x & 63) == 63;
@@ -389,6 +394,7 @@ __global__ __launch_bounds__(kThreads) void k_prefix_realign_np(PrefixRealignArg
 template <class T, class OP, int NP>
 __global__ __launch_bounds__(kThreads) void k_prefix_outshift(PrefixRealignArgs a, Geom g)
 {
+    if (g.acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
     constexpr int V = Pack<T>::N;
     const size_t nblk = gridDim.x;
     const unsigned d = a.d[0];

@@ -23,8 +23,9 @@ namespace sos {
 // first, then distance 1, 2, 4 pairs with the lower subtree the left operand).
 template <class T, class OP, int ORDER>
 __global__ __launch_bounds__(kThreads) void k_fold_dyn(T *out, FoldPtrs ins, int np,
-                                                         size_t n)
+                                                         size_t n, int acquire)
 {
+    if (acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
     const size_t stride = (size_t)gridDim.x * kThreads;
     int p2 = 1;
     while (p2 * 2 <= np) p2 *= 2;
@@ -98,8 +99,10 @@ int launch_fold_dyn(T *out, const FoldPtrs &ins, int np, size_t n, hipStream_t s
 {
     size_t blocks = (n + kThreads - 1) / kThreads;
     if (blocks > 8192) blocks = 8192;
+    const int acq = carry_acquire(st, (unsigned)blocks);
+    if (acq < 0) return SOSX_ERR_HIP;
     hipLaunchKernelGGL((k_fold_dyn<T, OP, ORDER>), dim3((unsigned)blocks), dim3(kThreads), 0, st, out, ins,
-                       np, n);
+                       np, n, acq);
     return hip_ok(hipGetLastError());
 }
 
@@ -122,6 +125,8 @@ int launch_fold_realign(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
         same &= a.d[k] == a.d[0];
     }
     const unsigned lds = np >= 5 ? occupancy_lds(np + 1) : 0u;  // the bench A/B only
+    g.acquire = carry_acquire(st, grid_for(g, kNoCap));
+    if (g.acquire < 0) return SOSX_ERR_HIP;
     if (same && a.d[0] != 0 && outshift_mode() != 0)
         hipLaunchKernelGGL((k_fold_outshift<T, OP, NP, ORDER>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
                            outshift_mode() == 2 ? lds : 0u, st, out, a, g);
@@ -151,6 +156,8 @@ int launch_fold_np(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
     if (!congruent || n * sizeof(T) <= kSpreadBytes) return launch_fold_dyn<T, OP, ORDER>(out, ins, NP, n, st);
     constexpr int U = NP <= 2 ? 4 : (NP <= 4 ? 2 : 1);
     Geom g = make_geom(o, n, sizeof(T), U);
+    g.acquire = carry_acquire(st, grid_for(g, kNoCap));
+    if (g.acquire < 0) return SOSX_ERR_HIP;
     hipLaunchKernelGGL((k_fold<T, OP, NP, ORDER, U>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
                        U == 1 ? occupancy_lds(NP + 1) : 0u, st, out, ins, g);
     return hip_ok(hipGetLastError());

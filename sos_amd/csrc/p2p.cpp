@@ -50,6 +50,7 @@
 #include <tuple>
 #include <vector>
 
+#include "carry.h"
 #include "p2p_proto.h"
 #include "plan.h"
 #include "runtime.h"
@@ -222,42 +223,34 @@ uint64_t team_word_get(int which, int world_pe)
 
 namespace {
 
-// One round's local ops (copies, zero fills, folds, prefixes); fold/prefix inputs come
-// from `ins` (received chunks may point into peer memory).
-int run_round_ops(const sosplan::Round &r, const std::vector<std::vector<const void *>> &ins,
-                  const std::function<char *(int, uint64_t)> &local_ptr, int op, int dt,
-                  hipStream_t stream)
+// One local op of a round (copy, zero fill, fold, prefix); fold/prefix inputs come from
+// `in` (received chunks may point into peer memory).
+int run_round_op(const sosplan::Local &l, const std::vector<const void *> &in,
+                 const std::function<char *(int, uint64_t)> &local_ptr, int op, int dt,
+                 hipStream_t stream)
 {
-    for (size_t i = 0; i < r.ops.size(); ++i) {
-        const auto &l = r.ops[i];
-        if (l.kind == sosplan::COPY) {
-            if (ins[i][0] != local_ptr(l.out_buf, l.out_off) &&
-                hipMemcpyAsync(local_ptr(l.out_buf, l.out_off), ins[i][0], l.count,
-                               hipMemcpyDeviceToDevice, stream) != hipSuccess)
-                return SOSX_ERR_HIP;
-            continue;
-        }
-        if (l.kind == sosplan::ZERO) {
-            if (hipMemsetAsync(local_ptr(l.out_buf, l.out_off), 0, l.count, stream) != hipSuccess)
-                return SOSX_ERR_HIP;
-            continue;
-        }
-        if (l.kind == sosplan::PREFIX) {
-            void *outs[sosplan::PLAN_MAX_PE];
-            for (int k = 0; k < l.nout; ++k) outs[k] = local_ptr(l.outs_buf[k], l.outs_off[k]);
-            prof_mark(0, false, stream);
-            int rc = sosx_prefix(op, dt, outs, ins[i].data(), l.nin, l.own, l.count, stream);
-            prof_mark(0, true, stream);
-            if (rc) return rc;
-            continue;
-        }
-        prof_mark(0, false, stream);
-        int rc = sosx_fold(op, dt, l.order, local_ptr(l.out_buf, l.out_off), ins[i].data(), l.nin,
-                           l.count, stream);
-        prof_mark(0, true, stream);
-        if (rc) return rc;
+    if (l.kind == sosplan::COPY) {
+        if (in[0] == local_ptr(l.out_buf, l.out_off)) return SOSX_OK;
+        if (sos::carry_acquire(stream, 0, false) < 0) return SOSX_ERR_HIP;  // a library copy
+        return hipMemcpyAsync(local_ptr(l.out_buf, l.out_off), in[0], l.count, hipMemcpyDeviceToDevice,
+                              stream) == hipSuccess
+                   ? SOSX_OK
+                   : SOSX_ERR_HIP;
     }
-    return SOSX_OK;
+    if (l.kind == sosplan::ZERO)
+        return hipMemsetAsync(local_ptr(l.out_buf, l.out_off), 0, l.count, stream) == hipSuccess ? SOSX_OK
+                                                                                                 : SOSX_ERR_HIP;
+    prof_mark(0, false, stream);
+    int rc;
+    if (l.kind == sosplan::PREFIX) {
+        void *outs[sosplan::PLAN_MAX_PE];
+        for (int k = 0; k < l.nout; ++k) outs[k] = local_ptr(l.outs_buf[k], l.outs_off[k]);
+        rc = sosx_prefix(op, dt, outs, in.data(), l.nin, l.own, l.count, stream);
+    } else {
+        rc = sosx_fold(op, dt, l.order, local_ptr(l.out_buf, l.out_off), in.data(), l.nin, l.count, stream);
+    }
+    prof_mark(0, true, stream);
+    return rc;
 }
 
 }  // namespace
@@ -387,10 +380,30 @@ bool in_peer_heap(const void *p)
     return false;
 }
 
+// The stream-wide acquire with the runtime's bookkeeping (carry.h stream_wide).
+int stream_wide_acquire(hipStream_t st) { return acquire_system(st) == hipSuccess ? 0 : 1; }
+
+// One p2p call's hand-off of the consumer-side acquire (carry.h): nothing owed at entry
+// or exit, the runtime's acquire kernel as the stream-wide form.
+struct CarryScope {
+    CarryScope() { reset(); }
+    ~CarryScope() { reset(); }
+    static void reset()
+    {
+        sos::AcquireCarry &c = sos::acquire_carry();
+        c.want = false;
+        c.peer = false;
+        c.stream_wide = &stream_wide_acquire;
+    }
+};
+
 // The protocol's backend on this PE's HIP stream (p2p_proto.h), both signalling modes.
 // It classifies waits and launches itself for the consumer-side check (note_peer_wait /
 // note_peer_read, runtime.h): a wait on a `posted` / `dposted` counter is a wait for a
-// peer's bytes; a gather or fold reading a peer's heap is a peer read.
+// peer's bytes; a gather or fold reading a peer's heap is a peer read.  acquire() does
+// not launch: it marks the acquire owed (carry.h), and the next launch that reads a
+// peer's heap carries it in its workgroups when its grid is small, or runs the acquire
+// kernel first; a read that did neither after a wait counts as unacquired.
 struct HipBackend {
     hipStream_t stream;
     int op, dt;
@@ -410,7 +423,20 @@ struct HipBackend {
         }();
         if (skip) return 0;
 #endif
-        return acquire_system(stream) == hipSuccess ? 0 : 1;
+        sos::acquire_carry().want = true;
+        return 0;
+    }
+    // a launch that reads peer bytes or not (`peer`): mark it for the launchers, then
+    // count the read -- acquired in its own workgroups if any of its launches carried
+    template <class F> int peer_launch(bool peer, F &&launch)
+    {
+        sos::AcquireCarry &c = sos::acquire_carry();
+        c.peer = peer;
+        const long c0 = c.carried;
+        const int rc = launch();
+        c.peer = false;
+        if (peer) note_peer_read(c.carried > c0);
+        return rc;
     }
     bool device_data_wait(int nq, const uint64_t *const *qa)
     {
@@ -422,9 +448,8 @@ struct HipBackend {
     {
         bool peer = false;
         for (int i = 0; i < n; ++i) peer |= in_peer_heap(srcs[i]);
-        if (peer) note_peer_read(false);
         prof_mark(1, false, stream);
-        const int rc = sosx_gather(n, srcs, dsts, bytes, stream);
+        const int rc = peer_launch(peer, [&] { return sosx_gather(n, srcs, dsts, bytes, stream); });
         prof_mark(1, true, stream);
         return rc;
     }
@@ -440,27 +465,30 @@ struct HipBackend {
                          const uint64_t *qv)
     {
         // the step's waits run inside the launch; with a wait for peers' bytes every
-        // workgroup acquires before its loads (copy.hip k_gather<true>)
+        // workgroup acquires before its loads (copy.hip k_gather<true>), or -- a step too
+        // large to ride in the copy -- the copies carry the acquire after it
         const bool own = device_data_wait(nq, qa);
         if (own) note_peer_wait();
         bool peer = false;
         for (int i = 0; i < n; ++i) peer |= in_peer_heap(srcs[i]);
-        if (peer) note_peer_read(own);
         prof_mark(1, false, stream);
-        const int rc = sosx_gather_signalled(n, srcs, dsts, bytes, nw, wa, wv, nq, qa, qv,
-                                             dev(&shared()->sig_err[my_world]), g_sig.limit_ticks, stream);
+        const int rc = peer_launch(peer, [&] {
+            return sosx_gather_signalled(n, srcs, dsts, bytes, nw, wa, wv, nq, qa, qv,
+                                         dev(&shared()->sig_err[my_world]), g_sig.limit_ticks, stream);
+        });
         prof_mark(1, true, stream);
         return rc;
     }
     int run_ops(const sosplan::Round &r, const std::vector<std::vector<const void *>> &ins,
                 const sosp2p::LocalPtr &local_ptr)
     {
-        for (const auto &in : ins) {
+        for (size_t i = 0; i < r.ops.size(); ++i) {
             bool peer = false;
-            for (const void *p : in) peer |= in_peer_heap(p);
-            if (peer) note_peer_read(false);
+            for (const void *p : ins[i]) peer |= in_peer_heap(p);
+            const int rc = peer_launch(peer, [&] { return run_round_op(r.ops[i], ins[i], local_ptr, op, dt, stream); });
+            if (rc) return rc;
         }
-        return run_round_ops(r, ins, local_ptr, op, dt, stream);
+        return SOSX_OK;
     }
     uint64_t *dev(uint64_t *p) { return sosrt::dev(p); }
     const uint64_t *dev(const uint64_t *p) { return sosrt::dev(p); }
@@ -504,6 +532,7 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
     if (!sh) return SOSX_ERR_STATE;
     const bool tr = trace_on();
     HipBackend be{stream, op, dt, t.world_rank(t.my_idx), tr ? now_s() : 0, tr};
+    CarryScope carry_scope;
     const sosp2p::Bufs pb{b.src, b.dst, b.scr, b.src_off, b.dst_off, b.scr_off, b.smis, b.dmis};
     auto world_of = [&](int i) { return t.world_rank(i); };
     if (g_sig.on) {

@@ -543,6 +543,7 @@ hipError_t acquire_system(hipStream_t stream)
         if (e != hipSuccess) return e;
     }
     ++s.sys_acquires;
+    ++s.acquire_kernels;
     s.acq_pending = false;
     return sosx_acquire_system(s.acq_mask, stream) == SOSX_OK ? hipSuccess : hipErrorLaunchFailure;
 }
@@ -1139,6 +1140,8 @@ void sosx_acquire_stats(long *acquires, long *peer_reads, long *unacquired, unsi
             (void)hipMemcpy(xcc_mask, s.acq_mask, sizeof(unsigned), hipMemcpyDeviceToHost);
     }
 }
+
+long sosx_acquire_kernels(void) { return st().acquire_kernels; }
 
 // Return this PE's private device workspaces (exchange scratch, staging for host
 // operands) to the runtime after the library stream drains; the next call that needs one

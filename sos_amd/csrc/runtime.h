@@ -89,6 +89,7 @@ struct State {
     long sys_releases = 0;            // how many sync_system / release_system markers ran
     // consumer half of the visibility rule (acquire_system, note_peer_wait/read)
     long sys_acquires = 0, peer_reads = 0, peer_reads_unacquired = 0;
+    long acquire_kernels = 0;         // of sys_acquires: stream-wide acquire kernels
     bool acq_pending = false;         // a peer wait since the last acquire (stream order)
     unsigned *acq_mask = nullptr;     // device word: XCD ids the acquire kernels ran on
     void *stripes = nullptr;

@@ -31,14 +31,7 @@ namespace sos {
 // MAXP = 8 for the P2 <= 8 kernels (one PE per GPU on a node): 150 B of kernel
 // arguments instead of 1 KiB, which the host launch call copies every time
 // (SOSX_SMALL_TRACE measured the launch call at 3.0 us with the 1 KiB block).
-__device__ __forceinline__ void slot_acquire()
-{
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: buffer_inv sc0 sc1
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-}
+__device__ __forceinline__ void slot_acquire() { wg_acquire(); }
 
 template <int MAXP> struct SmallFoldArgsT {
     const void *leaf[MAXP];

@@ -11,7 +11,10 @@ acquires, and left the unacquired count at 0 -- reductions under four schedules 
 p2p signalling modes at 1Mi + 3 elements and under two at 16Ki + 3 (gathers small enough
 to carry their signalling step), a scan, a broadcast, and the small path with host and
 device operands -- and that every result is the oracle's, read back by a plain D2H copy
-(tests/readback.py).  Prints one line per PE with the XCD mask of the acquire kernels.
+(tests/readback.py).  Small consuming grids carry the acquire in their own workgroups
+(carry.h): the 16Ki + 3 calls must run no acquire kernel at all, and an 8Mi + 3 call,
+whose folds stream, must run them.  Prints one line per PE with the XCD mask of the
+acquire kernels.
 
 Test infrastructure: the oracle is the checker only.
 """
@@ -46,12 +49,16 @@ def main():
     dt, op = L.dtype_id("float"), L.op_id("sum")
     bad, calls = [], 0
 
-    def call(what, fn, exp=None, got=None, reads=True):
+    def call(what, fn, exp=None, got=None, reads=True, kernels=None):
         nonlocal calls
         a0, r0, u0, _ = stats()
+        k0 = L.lib().sosx_acquire_kernels()
         fn()
         a1, r1, u1, _ = stats()
+        k1 = L.lib().sosx_acquire_kernels()
         calls += 1
+        if kernels is not None and (k1 > k0) != kernels:
+            bad.append((what, f"{k1 - k0} acquire kernels, expected {'some' if kernels else 'none'}"))
         if reads and r1 <= r0:
             bad.append((what, "no launch read a peer's bytes"))
         if reads and a1 <= a0:
@@ -65,8 +72,9 @@ def main():
 
     # the executors: device-heap operands past the small paths
     n = (1 << 20) + 3
-    dsrc = S.shmemx_malloc_device(n * 4)
-    ddst = S.shmemx_malloc_device(n * 4)
+    big = (8 << 20) + 3
+    dsrc = S.shmemx_malloc_device(big * 4)
+    ddst = S.shmemx_malloc_device(big * 4)
     ins = [O.fill(dt, 0, 91, q, n) for q in range(P)]
     L.check(L.lib().sosx_memcpy(dsrc, ins[me].ctypes.data, n * 4, None), "sosx_memcpy")
     dget = lambda: R.device_bytes(ddst, n * 4)  # noqa: E731
@@ -84,8 +92,16 @@ def main():
              O.scan(op, dt, ins, False)[me], dget, reads=me != 0)
         call(f"broadcast signal {mode}", lambda: S.shmem_float_broadcast(world, ddst, dsrc, n, 0),
              ins[0], dget, reads=me != 0)
+    # streaming folds (8Mi + 3 elements): the acquire kernel before them
+    bins = [O.fill(dt, 0, 94, q, big) for q in range(P)]
+    L.check(L.lib().sosx_memcpy(dsrc, bins[me].ctypes.data, big * 4, None), "sosx_memcpy")
+    bexp = O.ring(op, dt, bins)[me]
+    for mode in modes:
+        call(f"big ring signal {mode}", lambda: S.shmem_float_sum_reduce(world, ddst, dsrc, big), bexp,
+             lambda: R.device_bytes(ddst, big * 4), kernels=True)
     # mid-size device operands (past SHMEMX_SMALL_DEVICE, gathers of <= 256 KiB): in stream
-    # mode the signalling step rides in the gather launch, which acquires per workgroup
+    # mode the signalling step rides in the gather launch, which acquires per workgroup;
+    # every consuming launch is small enough to carry the acquire (no acquire kernel)
     mid = 16384 + 3
     mins = [O.fill(dt, 0, 93, q, mid) for q in range(P)]
     L.check(L.lib().sosx_memcpy(dsrc, mins[me].ctypes.data, mid * 4, None), "sosx_memcpy")
@@ -95,7 +111,7 @@ def main():
             res = S.lib().sosx_resolve_alg(L.ALGS[alg], mid * 4, 16384)
             exp = (O.ring(op, dt, mins) if res == L.ALGS["ring"] else O.recdbl(op, dt, mins))[me]
             call(f"mid {alg} signal {mode}", lambda: S.shmem_float_sum_reduce(world, ddst, dsrc, mid), exp,
-                 lambda: R.device_bytes(ddst, mid * 4))
+                 lambda: R.device_bytes(ddst, mid * 4), kernels=False)
     S.shmemx_set_reduce_algorithm(L.ALGS["auto"])
     # the small path: host-heap operands, then small device-heap operands
     m = 64
@@ -122,7 +138,7 @@ def main():
         print(f"PE {me}/{P}: {len(bad)} of {calls} calls FAILED: {bad[:6]}", flush=True)
         return 1
     print(f"PE {me}/{P}: {calls} calls, {reads} peer reads, {acq} acquires, {unacq} unacquired, "
-          f"xcc mask 0x{mask:02x}", flush=True)
+          f"{L.lib().sosx_acquire_kernels()} acquire kernels, xcc mask 0x{mask:02x}", flush=True)
     return 0
 
 

@@ -297,6 +297,59 @@ int main(int argc, char **argv)
                    ms * 1e3 / K, std::chrono::duration<double, std::micro>(w1 - w0).count() / K);
         }
     }
+    // the acquire kernel's grid: 8 / 16 / 64 one-wave workgroups (XCD mask of each)
+    for (int rep = 0; rep < 2; ++rep) {
+        for (unsigned wgs : {8u, 16u, 64u}) {
+            const int K = 200;
+            CK(hipMemset(mask, 0, 4));
+            CK(hipStreamSynchronize(s));
+            CK(hipEventRecord(e0, s));
+            for (int k = 0; k < K; ++k) {
+                hipLaunchKernelGGL(k_acquire, dim3(wgs), dim3(64), 0, s, mask);
+                hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
+            }
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            unsigned m = 0;
+            CK(hipMemcpy(&m, mask, 4, hipMemcpyDeviceToHost));
+            printf("empty-kernel chain, acquire kernel of %2u workgroups before each: %.2f us per step, xcc mask 0x%02x\n",
+                   wgs, ms * 1e3 / K, m);
+        }
+    }
+    // a small consumer of G workgroups (one 4 KiB tile each): no acquire, the acquire kernel
+    // before it, or each workgroup's own acquire -- in a chain and from an idle stream
+    const char *forms[] = {"no acquire", "acquire kernel first", "acquire in each workgroup"};
+    for (int rep = 0; rep < 2; ++rep) {
+        for (unsigned G : {1u, 16u, 64u, 256u, 1024u}) {
+            for (int f = 0; f < 3; ++f) {
+                const int K = 200;
+                auto launch = [&] {
+                    if (f == 1) hipLaunchKernelGGL(k_acquire, dim3(64), dim3(64), 0, s, mask);
+                    if (f == 2) hipLaunchKernelGGL(k_stream<true>, dim3(G), dim3(256), 0, s, a, o, (size_t)G * 256);
+                    else hipLaunchKernelGGL(k_stream<false>, dim3(G), dim3(256), 0, s, a, o, (size_t)G * 256);
+                };
+                CK(hipStreamSynchronize(s));
+                CK(hipEventRecord(e0, s));
+                for (int k = 0; k < K; ++k) launch();
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                double tot = 0;
+                for (int k = 0; k < K; ++k) {
+                    CK(hipStreamSynchronize(s));
+                    auto w0 = std::chrono::steady_clock::now();
+                    launch();
+                    CK(hipStreamSynchronize(s));
+                    tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count();
+                }
+                printf("consumer of %4u workgroups, %-26s chain %.2f us per step, idle stream %.2f us host wall\n",
+                       G, forms[f], ms * 1e3 / K, tot / K);
+            }
+        }
+    }
     // one call's worth from an idle stream: host waits, then [acquire] + kernel + sync
     for (int rep = 0; rep < 2; ++rep) {
         for (int acq = 0; acq < 3; ++acq) {
