@@ -214,6 +214,15 @@ __device__ __forceinline__ u32x4 ldv(const u32x4 *p)
     if constexpr (NT) return __builtin_nontemporal_load(p);
     else return *p;
 }
+// A 16-B nontemporal load from an address that is only element-aligned (4 or 8 B): one
+// global_load_dwordx4, which the memory pipeline splits where it straddles (ROCm runs the
+// GPU in unaligned-access mode).  It reads exactly the 16 bytes asked for.
+typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ u32x4 ldv_unaligned(const void *p)
+{
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4u *>(p));
+}
+
 template <bool NT>
 __device__ __forceinline__ void stv(u32x4 *p, u32x4 v)
 {

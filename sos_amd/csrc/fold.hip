@@ -109,8 +109,14 @@ struct PrefixFn {
                         a.d[k] = (unsigned)((uintptr_t)((const T *)p->in[k] + g.head) & 15);
                     }
                     bool same = true;
-                    for (int k = 0; k < np; ++k) same &= a.d[k] == a.d[0];
+                    int m = 0;  // incongruent inputs
+                    for (int k = 0; k < np; ++k) {
+                        same &= a.d[k] == a.d[0];
+                        m += a.d[k] != 0;
+                    }
                     const bool outshift = same && a.d[0] != 0 && prefix_outshift_on();
+                    constexpr bool kUL = sizeof(T) == 4 || sizeof(T) == 8;
+                    const bool ul = kUL && !outshift && m >= realign_unaligned_min();
                     g.acquire = carry_acquire(st, grid_for(g, kNoCap));
                     if (g.acquire < 0) return SOSX_ERR_HIP;
                     switch (np) {
@@ -119,6 +125,9 @@ struct PrefixFn {
         if (outshift)                                                                                      \
             hipLaunchKernelGGL((k_prefix_outshift<T, OP, P>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0u, \
                                st, a, g);                                                                  \
+        else if (ul)                                                                                       \
+            hipLaunchKernelGGL((k_prefix_realign_np<T, OP, P, kUL>), dim3(grid_for(g, kNoCap)), dim3(kThreads), \
+                               0u, st, a, g);                                                              \
         else                                                                                               \
             hipLaunchKernelGGL((k_prefix_realign_np<T, OP, P>), dim3(grid_for(g, kNoCap)), dim3(kThreads), \
                                0u, st, a, g);                                                              \

@@ -151,8 +151,12 @@ __device__ __forceinline__ T fold_runtime_np_elem(const FoldRealignArgs &a, size
 // incongruent (profiles/r6_realign_pmc.txt).  Over 1..8 incongruent inputs of 8 x 16Mi
 // fp32 (tools/realign_ab.py, profiles/r6_realign_ab.txt) this shape is the fastest or
 // within 1 % up to 6 (m = 1 6.21, m = 3 6.10, m = 6 5.64 TB/s against 6.22 / 5.68 / 5.05
-// for round 5's) and 2 % behind plain double loads at 8.
-template <class T, class OP, int NP, int ORDER>
+// for round 5's) and 2 % behind plain double loads at 8.  UL (elements of 4 or 8 bytes,
+// most inputs incongruent): one unaligned 16-B load per input and lane instead, no DPP and
+// no shift -- flat at 5.84-5.95 TB/s however many inputs are incongruent, against 5.03-5.11
+// for the DPP shape with all 8 at mixed offsets and 5.37-5.64 with 6 of 8
+// (profiles/r6_realign_unaligned.txt); the DPP shape stays ahead up to 4 of 8.
+template <class T, class OP, int NP, int ORDER, bool UL = false>
 __global__ __launch_bounds__(kThreads) void k_fold_realign_np(T *out, FoldRealignArgs a, Geom g)
 {
     if (g.acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
@@ -167,6 +171,12 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_np(T *out, FoldRealig
     for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
         const size_t i = t * (size_t)kThreads + threadIdx.x;
         u32x4 x[NP], y[NP];
+        if constexpr (UL) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) x[k] = ldv_unaligned(reinterpret_cast<const char *>(I[k] + i) + a.d[k]);
+            stv<true>(O + i, fold_pack<T, OP, NP, ORDER>(x));
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < NP; ++k) x[k] = ldv<true>(I[k] + i);
         if (last_lane) {  // its next vector belongs to the next wave (or workgroup)
@@ -245,6 +255,18 @@ inline unsigned occupancy_lds(int streams)
     if (streams >= 12) return 64u << 10;  // 2 workgroups per CU
     if (streams >= 4) return 48u << 10;   // 3 per CU
     return 0;
+}
+
+// The realigning fold / prefix take the unaligned-load form (UL) when at least this many
+// inputs are incongruent (elements of 4 or 8 bytes).  Bench switch SOSX_REALIGN_UNALIGNED
+// = the count (1: whenever one is; 9: never); both forms are bit-exact.
+inline int realign_unaligned_min()
+{
+    static const int m = [] {
+        const char *e = getenv("SOSX_REALIGN_UNALIGNED");
+        return e && *e ? atoi(e) : 5;
+    }();
+    return m;
 }
 
 // The fold of one element order over any (type, op) (fold_order.hip, one object per
@@ -328,8 +350,8 @@ struct PrefixRealignArgs {
 // vectors), the other lanes' next vectors by DPP from the neighbouring lane (round 6, as
 // k_fold_realign_np: round 5's second load per lane read 1.42x the algorithmic bytes,
 // profiles/r6_realign_pmc.txt), then the prefix.  Every load of the tile still precedes
-// the first store (aliasing, as k_prefix).
-template <class T, class OP, int NP>
+// the first store (aliasing, as k_prefix).  UL: unaligned loads, as k_fold_realign_np.
+template <class T, class OP, int NP, bool UL = false>
 __global__ __launch_bounds__(kThreads) void k_prefix_realign_np(PrefixRealignArgs a, Geom g)
 {
     if (g.acquire) wg_acquire();  // a small grid reading a peer's bytes (carry_acquire)
@@ -346,20 +368,25 @@ __global__ __launch_bounds__(kThreads) void k_prefix_realign_np(PrefixRealignArg
     for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
         const size_t i = t * (size_t)kThreads + threadIdx.x;
         u32x4 x[NP], y[NP];
+        if constexpr (UL) {
 #pragma unroll
-        for (int k = 0; k < NP; ++k) x[k] = ldv<true>(I[k] + i);
-        if (last_lane) {
+            for (int k = 0; k < NP; ++k) x[k] = ldv_unaligned(reinterpret_cast<const char *>(I[k] + i) + a.d[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) x[k] = ldv<true>(I[k] + i);
+            if (last_lane) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k)
+                    if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
+            }
 #pragma unroll
             for (int k = 0; k < NP; ++k)
-                if (a.d[k]) y[k] = ldv<true>(I[k] + i + 1);
+                if (a.d[k]) {
+                    const u32x4 nx = next_lane16(x[k]);
+                    if (!last_lane) y[k] = nx;
+                    x[k] = realign16(x[k], y[k], a.d[k]);
+                }
         }
-#pragma unroll
-        for (int k = 0; k < NP; ++k)
-            if (a.d[k]) {
-                const u32x4 nx = next_lane16(x[k]);
-                if (!last_lane) y[k] = nx;
-                x[k] = realign16(x[k], y[k], a.d[k]);
-            }
         u32x4 acc = x[0];
         stv<true>(O[0] + i, acc);
 #pragma unroll

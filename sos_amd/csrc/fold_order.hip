@@ -119,10 +119,12 @@ int launch_fold_realign(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
     memset(&a, 0, sizeof(a));
     a.np = np;
     bool same = true;  // every input at one offset: realign the output instead
+    int m = 0;         // incongruent inputs
     for (int k = 0; k < np; ++k) {
         a.p[k] = ins.p[k];
         a.d[k] = (unsigned)((uintptr_t)((const T *)ins.p[k] + g.head) & 15);
         same &= a.d[k] == a.d[0];
+        m += a.d[k] != 0;
     }
     const unsigned lds = np >= 5 ? occupancy_lds(np + 1) : 0u;  // the bench A/B only
     g.acquire = carry_acquire(st, grid_for(g, kNoCap));
@@ -130,6 +132,9 @@ int launch_fold_realign(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
     if (same && a.d[0] != 0 && outshift_mode() != 0)
         hipLaunchKernelGGL((k_fold_outshift<T, OP, NP, ORDER>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
                            outshift_mode() == 2 ? lds : 0u, st, out, a, g);
+    else if ((sizeof(T) == 4 || sizeof(T) == 8) && m >= realign_unaligned_min())
+        hipLaunchKernelGGL((k_fold_realign_np<T, OP, NP, ORDER, (sizeof(T) == 4 || sizeof(T) == 8)>),
+                           dim3(grid_for(g, kNoCap)), dim3(kThreads), 0u, st, out, a, g);
     else
         hipLaunchKernelGGL((k_fold_realign_np<T, OP, NP, ORDER>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0u,
                            st, out, a, g);

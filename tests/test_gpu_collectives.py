@@ -183,6 +183,24 @@ def test_fold_realigned_inputs(torch_cuda, P, dt, op, layout, order):
         assert np.array_equal(bits(from_dev(out, ref)), bits(ref)), (n, offs)
 
 
+@pytest.mark.parametrize("form", ["1", "9"])
+def test_realign_forms_forced(form):
+    """Both forms of the realigning fold and prefix, bit for bit: SOSX_REALIGN_UNALIGNED=1
+    sends every layout with an incongruent input to the unaligned-load form (by default only
+    5 or more of them, fp32/fp64/int32/int64), =9 keeps every layout on the DPP form; the
+    realigned-input tests above rerun in a child process under each setting."""
+    import subprocess
+    import sys
+    here = os.path.abspath(__file__)
+    env = dict(os.environ, SOSX_REALIGN_UNALIGNED=form)
+    r = subprocess.run([sys.executable, "-m", "pytest", here, "-q", "-p", "no:cacheprovider", "-k",
+                        "(test_fold_realigned_inputs and (own or mixed)) or test_prefix_realigned_inputs"],
+                       capture_output=True, text=True, timeout=280, env=env,
+                       cwd=os.path.dirname(os.path.dirname(here)))
+    assert r.returncode == 0, (r.stdout[-2500:], r.stderr[-1500:])
+    assert " passed" in r.stdout and "failed" not in r.stdout
+
+
 def test_fold_selection_exits_cleanly():
     """The float-sum runtime-P fold selection used to abort at interpreter exit (two HIP
     runtimes in one process); the selection must now exit with status 0."""

@@ -356,8 +356,11 @@ __global__ __launch_bounds__(kThreads) void k_prefix_buf(PrefixPtrs p, Geom g)
 // line the first load brought into L2); MODE 2: both loads plain; MODE 3: the second
 // vector from the next lane by DPP wave_shl:1 (lane 63 loads it); MODE 4: the same through
 // __shfl_down; MODE 5: two loads, plain for the incongruent inputs and nt for the
-// congruent ones; MODE 6: plain loads + DPP; MODE 7: MODE 5's policy + DPP.  Same element
-// order as k_fold_realign_np.
+// congruent ones; MODE 6: plain loads + DPP; MODE 7: MODE 5's policy + DPP; MODE 8: DPP
+// + LDS across waves; MODE 9 / 10: one unaligned 16-B load per lane (nt / plain).  Same
+// element order as k_fold_realign_np.
+typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(4)));
+
 template <class T, class OP, int NP, int ORDER, int MODE>
 __global__ __launch_bounds__(kThreads) void k_fold_realign_v(T *out, FoldRealignArgs a, Geom g)
 {
@@ -372,7 +375,19 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_v(T *out, FoldRealign
         const size_t i = t * (size_t)kThreads + threadIdx.x;
         u32x4 x[NP], y[NP];
         constexpr bool kSplit = MODE == 5 || MODE == 7;  // nt only for congruent inputs
-        constexpr bool kNt = MODE == 0 || MODE == 1 || MODE == 3 || MODE == 4 || MODE == 8;
+        constexpr bool kNt = MODE == 0 || MODE == 1 || MODE == 3 || MODE == 4 || MODE == 8 || MODE == 9;
+        if constexpr (MODE == 9 || MODE == 10) {
+            // one 16-B load per lane straight from the element-aligned (4-B) address: the
+            // memory pipeline splits what straddles, no second vector, no shift
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const u32x4u *p = reinterpret_cast<const u32x4u *>(reinterpret_cast<const char *>(I[k] + i) + a.d[k]);
+                if constexpr (MODE == 9) x[k] = __builtin_nontemporal_load(p);
+                else x[k] = *p;
+            }
+            stv<true>(O + i, fold_pack<T, OP, NP, ORDER>(x));
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
             if constexpr (kSplit) x[k] = a.d[k] ? ldv<false>(I[k] + i) : ldv<true>(I[k] + i);
@@ -923,6 +938,8 @@ int sosxv_fold_realign(int mode, void *out, const void *const *ins, size_t n, vo
         case 6: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 6>), grid, blk, 0, st, (float *)out, a, g); break;
         case 7: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 7>), grid, blk, 0, st, (float *)out, a, g); break;
         case 8: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 8>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 9: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 9>), grid, blk, 0, st, (float *)out, a, g); break;
+        case 10: hipLaunchKernelGGL((k_fold_realign_v<float, OpSum, 8, SOSX_ORDER_LINEAR, 10>), grid, blk, 0, st, (float *)out, a, g); break;
         default: return SOSX_ERR_ARG;
     }
     return hip_ok(hipGetLastError());
