@@ -58,16 +58,20 @@ using namespace sos;
 
 namespace {
 
-// Bench switch: SOSX_PREFIX_OUTSHIFT=0 sends the one-offset case to k_prefix_realign_np
-// (profiles/r5_fold_outshift.txt; both bit-exact).  Neither prefix shape takes the
-// occupancy cap: it measured neutral (k_prefix_realign_np: -1..+0 %).
-inline bool prefix_outshift_on()
+// Bench switch for the one-offset case (all bit-exact): unset, the unaligned-load form
+// for 4- and 8-byte elements at P = 1 and P >= 5, k_prefix_outshift otherwise; =1
+// k_prefix_outshift always, =0 k_prefix_realign_np (DPP or UL by the incongruent count).
+// P x 16Mi fp32 at +4 / +8 (profiles/r6_outshift_ab.txt): UL 6.14-6.24 / 5.75-5.81 TB/s at
+// P = 1 / 8 against outshift's 5.82-5.99 / 5.37-5.40; at P = 2 / 3 the two tie, at P = 4
+// outshift leads (5.94-6.01 against 5.79-5.85).  Neither prefix shape takes the occupancy
+// cap: it measured neutral (k_prefix_realign_np: -1..+0 %).
+inline int prefix_outshift_mode()
 {
-    static const bool on = [] {
+    static const int m = [] {
         const char *e = getenv("SOSX_PREFIX_OUTSHIFT");
-        return !(e && *e == '0');
+        return e && *e ? atoi(e) : -1;
     }();
-    return on;
+    return m;
 }
 
 template <class T, class OP, int NP>
@@ -114,9 +118,12 @@ struct PrefixFn {
                         same &= a.d[k] == a.d[0];
                         m += a.d[k] != 0;
                     }
-                    const bool outshift = same && a.d[0] != 0 && prefix_outshift_on();
                     constexpr bool kUL = sizeof(T) == 4 || sizeof(T) == 8;
-                    const bool ul = kUL && !outshift && m >= realign_unaligned_min();
+                    const bool one_offset = same && a.d[0] != 0;
+                    const int om = prefix_outshift_mode();
+                    const bool ul_one = kUL && (np == 1 || np >= 5);  // the one-offset auto choice
+                    const bool outshift = one_offset && (om > 0 || (om < 0 && !ul_one));
+                    const bool ul = kUL && !outshift && (m >= realign_unaligned_min() || (one_offset && om < 0));
                     g.acquire = carry_acquire(st, grid_for(g, kNoCap));
                     if (g.acquire < 0) return SOSX_ERR_HIP;
                     switch (np) {

@@ -79,17 +79,19 @@ namespace {
 // flight at once instead of one workgroup's; latency, not bandwidth, bounds these calls.
 constexpr size_t kSpreadBytes = 64 * 1024;
 
-// Bench switch (profiles/r5_fold_outshift.txt; every choice is bit-exact, only speed
-// differs): SOSX_FOLD_OUTSHIFT=0 sends the one-offset case to k_fold_realign_np, =2 runs
-// k_fold_outshift under the multi-stream occupancy cap.  The default (no cap) won:
-// 8 x 16Mi fp32 at +4 / +8 / +12 bytes 5.79-5.90 / 5.98-6.06 / 6.10-6.17 TB/s, capped
-// 5.21-5.27 / 5.52-5.57 / 5.54-5.59, k_fold_realign_np 4.16-4.23 / 4.26-4.43 / 4.35-4.44
-// (the runtime-P kernel before it: 3.22-3.26 / 3.37-3.39 / 3.31-3.32).
+// Bench switch for the one-offset case (every input at the same 16-B offset d != 0; every
+// choice is bit-exact, only speed differs).  Unset: the unaligned-load form for 4- and
+// 8-byte elements, k_fold_outshift for the others; =1 k_fold_outshift for every type, =2
+// the same under the multi-stream occupancy cap, =0 k_fold_realign_np (DPP or UL by the
+// incongruent count).  P x 16Mi fp32 at +4 / +8 (profiles/r6_outshift_ab.txt): the UL
+// form 6.52-6.63 / 6.50-6.57 / 6.13-6.28 / 6.06-6.10 TB/s at P = 2 / 3 / 4 / 8 against
+// outshift's 6.34-6.41 / 6.37-6.41 / 6.11-6.21 / 5.88-6.08.  Round 5 (r5_fold_outshift.txt):
+// outshift 5.79-6.17 beat the cap (5.21-5.59) and the two-load realign (4.16-4.44).
 inline int outshift_mode()
 {
     static const int m = [] {
         const char *e = getenv("SOSX_FOLD_OUTSHIFT");
-        return e && *e ? atoi(e) : 1;
+        return e && *e ? atoi(e) : -1;
     }();
     return m;
 }
@@ -107,9 +109,10 @@ int launch_fold_dyn(T *out, const FoldPtrs &ins, int np, size_t n, hipStream_t s
 }
 
 // Some inputs at another 16-B offset than the output (all element-aligned), either
-// order: 16-B vectors, realigned in registers (fold_kernels.h): the output when every
-// input sits at one offset, else each incongruent input.  No occupancy cap (both shapes
-// lost with it: profiles/r5_fold_outshift.txt).
+// order: 16-B vectors (fold_kernels.h), loaded unaligned (4- and 8-byte elements, every
+// input at one offset or at least realign_unaligned_min() inputs incongruent) or
+// realigned in registers (the output when every input sits at one offset, else each
+// incongruent input).  No occupancy cap (the shapes lost with it: r5_fold_outshift.txt).
 template <class T, class OP, int NP, int ORDER>
 int launch_fold_realign(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
 {
@@ -129,11 +132,14 @@ int launch_fold_realign(T *out, const FoldPtrs &ins, size_t n, hipStream_t st)
     const unsigned lds = np >= 5 ? occupancy_lds(np + 1) : 0u;  // the bench A/B only
     g.acquire = carry_acquire(st, grid_for(g, kNoCap));
     if (g.acquire < 0) return SOSX_ERR_HIP;
-    if (same && a.d[0] != 0 && outshift_mode() != 0)
+    constexpr bool kUL = sizeof(T) == 4 || sizeof(T) == 8;
+    const bool one_offset = same && a.d[0] != 0;
+    const int om = outshift_mode();
+    if (one_offset && (om > 0 || (om < 0 && !kUL)))
         hipLaunchKernelGGL((k_fold_outshift<T, OP, NP, ORDER>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
-                           outshift_mode() == 2 ? lds : 0u, st, out, a, g);
-    else if ((sizeof(T) == 4 || sizeof(T) == 8) && m >= realign_unaligned_min())
-        hipLaunchKernelGGL((k_fold_realign_np<T, OP, NP, ORDER, (sizeof(T) == 4 || sizeof(T) == 8)>),
+                           om == 2 ? lds : 0u, st, out, a, g);
+    else if (kUL && (m >= realign_unaligned_min() || (one_offset && om < 0)))
+        hipLaunchKernelGGL((k_fold_realign_np<T, OP, NP, ORDER, kUL>),
                            dim3(grid_for(g, kNoCap)), dim3(kThreads), 0u, st, out, a, g);
     else
         hipLaunchKernelGGL((k_fold_realign_np<T, OP, NP, ORDER>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0u,

@@ -183,18 +183,21 @@ def test_fold_realigned_inputs(torch_cuda, P, dt, op, layout, order):
         assert np.array_equal(bits(from_dev(out, ref)), bits(ref)), (n, offs)
 
 
-@pytest.mark.parametrize("form", ["1", "9"])
+@pytest.mark.parametrize("form", ["unaligned", "shifted"])
 def test_realign_forms_forced(form):
-    """Both forms of the realigning fold and prefix, bit for bit: SOSX_REALIGN_UNALIGNED=1
-    sends every layout with an incongruent input to the unaligned-load form (by default only
-    5 or more of them, fp32/fp64/int32/int64), =9 keeps every layout on the DPP form; the
+    """Every form of the realigning fold and prefix, bit for bit.  "unaligned": every layout
+    with an incongruent input takes the unaligned-load form (fp32/fp64/int32/int64; by
+    default only five or more incongruent inputs, or all at one offset); "shifted": the
+    register-realigned forms only (DPP per input, outshift for one-offset layouts).  The
     realigned-input tests above rerun in a child process under each setting."""
     import subprocess
     import sys
     here = os.path.abspath(__file__)
-    env = dict(os.environ, SOSX_REALIGN_UNALIGNED=form)
+    knobs = {"unaligned": ("1", "0"), "shifted": ("9", "1")}[form]
+    env = dict(os.environ, SOSX_REALIGN_UNALIGNED=knobs[0], SOSX_FOLD_OUTSHIFT=knobs[1],
+               SOSX_PREFIX_OUTSHIFT=knobs[1])
     r = subprocess.run([sys.executable, "-m", "pytest", here, "-q", "-p", "no:cacheprovider", "-k",
-                        "(test_fold_realigned_inputs and (own or mixed)) or test_prefix_realigned_inputs"],
+                        "test_fold_realigned_inputs or test_prefix_realigned_inputs"],
                        capture_output=True, text=True, timeout=280, env=env,
                        cwd=os.path.dirname(os.path.dirname(here)))
     assert r.returncode == 0, (r.stdout[-2500:], r.stderr[-1500:])

@@ -66,7 +66,7 @@ def fold(args):
     torch.cuda.set_device(0)
     S = torch.cuda.current_stream()
     st = S.cuda_stream
-    P, n, es = 8, 16 << 20, 4
+    P, n, es = args.np, 16 << 20, 4
     nb = n * es
     bufs = [torch.empty(nb + (1 << 20), dtype=torch.uint8, device="cuda") for _ in range(P + 1)]
     # page-aligned, 4 KiB colours apart (as the device heap places them); 1 MiB of slack
@@ -106,14 +106,14 @@ def prefix(args):
     torch.cuda.set_device(0)
     S = torch.cuda.current_stream()
     st = S.cuda_stream
-    P, n, es = 8, 16 << 20, 4
+    P, n, es = args.np, 16 << 20, 4
     nb = n * es
     bufs = [torch.empty(nb + (1 << 20), dtype=torch.uint8, device="cuda") for _ in range(2 * P)]
     base = [((b.data_ptr() + 4095) & ~4095) + 4096 * (k % 8) for k, b in enumerate(bufs)]
     outs = base[P:]
     out = {}
     for name, offs in (("congruent", [0] * P), ("input0+4", [4] + [0] * (P - 1)), ("all+4", [4] * P),
-                       ("mixed", [(4 * (k + 1)) % 16 for k in range(P)])):
+                       ("all+8", [8] * P), ("mixed", [(4 * (k + 1)) % 16 for k in range(P)])):
         if args.only and name not in args.only.split(","):
             continue
         ins = [base[k] + offs[k] for k in range(P)]
@@ -141,6 +141,7 @@ if __name__ == "__main__" and "--prefix" in sys.argv:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="", help="comma-separated layouts (default: all)")
+    ap.add_argument("--np", type=int, default=8, help="inputs (1..8)")
     prefix(ap.parse_args())
     sys.exit(0)
 
@@ -150,6 +151,7 @@ if __name__ == "__main__" and "--fold" in sys.argv:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="", help="comma-separated layouts (default: all)")
+    ap.add_argument("--np", type=int, default=8, help="inputs (2..8)")
     fold(ap.parse_args())
     sys.exit(0)
 
