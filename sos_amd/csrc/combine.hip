@@ -44,6 +44,17 @@ int launch_combine3_vec(T *out, const T *a, const T *b, size_t n, hipStream_t st
     return hip_ok(hipGetLastError());
 }
 
+// Bench switch SOSX_COMBINE_REALIGN (k_combine3_realign's MODE): 0 two aligned loads per
+// lane, 1 DPP, 2 unaligned loads (4- and 8-byte elements; others take 0).
+inline int combine_realign_mode()
+{
+    static const int m = [] {
+        const char *e = getenv("SOSX_COMBINE_REALIGN");
+        return e && *e ? atoi(e) : 0;
+    }();
+    return m;
+}
+
 template <class T, class OP>
 int launch_combine3(T *out, const T *a, const T *b, size_t n, hipStream_t st)
 {
@@ -57,8 +68,17 @@ int launch_combine3(T *out, const T *a, const T *b, size_t n, hipStream_t st)
         (pb % sizeof(T)) == 0) {
         Geom g = make_geom(o, n, sizeof(T), 1);
         const unsigned d = (unsigned)((uintptr_t)(b + g.head) & 15);
-        hipLaunchKernelGGL((k_combine3_realign<T, OP>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0,
-                           st, out, a, b, g, d);
+        constexpr bool kUL = sizeof(T) == 4 || sizeof(T) == 8;
+        const int mode = combine_realign_mode();
+        if (mode == 2 && kUL)
+            hipLaunchKernelGGL((k_combine3_realign<T, OP, kUL ? 2 : 0>), dim3(grid_for(g, kNoCap)), dim3(kThreads),
+                               0, st, out, a, b, g, d);
+        else if (mode == 1)
+            hipLaunchKernelGGL((k_combine3_realign<T, OP, 1>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0, st,
+                               out, a, b, g, d);
+        else
+            hipLaunchKernelGGL((k_combine3_realign<T, OP>), dim3(grid_for(g, kNoCap)), dim3(kThreads), 0,
+                               st, out, a, b, g, d);
         return hip_ok(hipGetLastError());
     }
     if (!congruent || sizeof(T) > 16) {

@@ -46,7 +46,9 @@ __global__ __launch_bounds__(kThreads) void k_combine3(T *out, const T *a,
 // at least one byte of b cannot cross a page boundary, and every load here does, so
 // reading the bytes shifted out is safe.  Same element operations as k_combine3.
 // ---------------------------------------------------------------------------------
-template <class T, class OP>
+// MODE 0: the two aligned loads per lane; 1: the next vector from the next lane (DPP,
+// lane 63 loads its own); 2: one unaligned 16-B load (4- and 8-byte elements).
+template <class T, class OP, int MODE = 0>
 __global__ __launch_bounds__(kThreads) void k_combine3_realign(T *out, const T *a, const T *b,
                                                                  Geom g, unsigned d)
 {
@@ -57,9 +59,19 @@ __global__ __launch_bounds__(kThreads) void k_combine3_realign(T *out, const T *
     u32x4 *O = reinterpret_cast<u32x4 *>(out + g.head);
     for (size_t t = blockIdx.x; t < g.tiles; t += nblk) {
         const size_t i = t * (size_t)kThreads + threadIdx.x;
-        const u32x4 ra = ldv<true>(A + i), lo = ldv<true>(B + i);
-        const u32x4 hi = ldv<true>(B + i + 1);
-        stv<true>(O + i, apply<T, OP>(ra, realign16(lo, hi, d)));
+        const u32x4 ra = ldv<true>(A + i);
+        if constexpr (MODE == 2) {
+            stv<true>(O + i, apply<T, OP>(ra, ldv_unaligned(reinterpret_cast<const char *>(B + i) + d)));
+        } else if constexpr (MODE == 1) {
+            const bool last_lane = (threadIdx.x & 63) == 63;
+            const u32x4 lo = ldv<true>(B + i);
+            u32x4 hi = next_lane16(lo);
+            if (last_lane) hi = ldv<true>(B + i + 1);
+            stv<true>(O + i, apply<T, OP>(ra, realign16(lo, hi, d)));
+        } else {
+            const u32x4 lo = ldv<true>(B + i), hi = ldv<true>(B + i + 1);
+            stv<true>(O + i, apply<T, OP>(ra, realign16(lo, hi, d)));
+        }
     }
     if (g.has_rem && blockIdx.x == nblk - 1) {
         for (size_t i = threadIdx.x; i < g.head; i += kThreads) out[i] = OP::f(a[i], b[i]);

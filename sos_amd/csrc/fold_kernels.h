@@ -206,6 +206,8 @@ __global__ __launch_bounds__(kThreads) void k_fold_realign_np(T *out, FoldRealig
 // per input per lane, and realign the OUTPUT: out vector i = realign16(F_i, F_i+1, d),
 // F_i+1 taken from the next lane (DPP); the last lane of each wave folds its F_i+1 itself
 // (k_fold_realign_np would load two vectors per input: 4.2-4.4 TB/s here, 5.8-6.1 this way).
+// Since round 6 only 1- and 2-byte elements take it by default: 4- and 8-byte ones load
+// unaligned (k_fold_realign_np UL, equal or faster at every P: profiles/r6_outshift_ab.txt).
 template <class T, class OP, int NP, int ORDER>
 __global__ __launch_bounds__(kThreads) void k_fold_outshift(T *out, FoldRealignArgs a, Geom g)
 {

@@ -161,8 +161,9 @@ def test_fold_realigned_inputs(torch_cuda, P, dt, op, layout, order):
     first, then the pairwise tree): the PE's own source chunk only ("own", the ring at PE
     me with source and target at different offsets), every input at one offset ("peers"
     at +8, "peers_es" at +element size: the p2p transport's in-place reads of the peers'
-    sources, k_fold_outshift realigning the output), or each input at its own offset
-    ("mixed"); ragged sizes; bit for bit against the plan simulator's fold."""
+    sources: unaligned loads for 4- and 8-byte elements, k_fold_outshift realigning the
+    output for the others), or each input at its own offset ("mixed"); ragged sizes; bit
+    for bit against the plan simulator's fold."""
     torch = torch_cuda
     es = O.lib().oracle_type_size(dt)
     for n in ((1 << 16) // es + 1, (1 << 20) + 3):
