@@ -142,6 +142,22 @@ def test_combine_realigned_every_offset(torch_cuda, sos, oracle, dt, op):
                 assert check(dt, op, from_dev(da, a_off, a), ref), f"n={n} a_off={a_off} d={d}"
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_combine_realign_shapes_forced(mode):
+    """The realigning combine's bench shapes (SOSX_COMBINE_REALIGN: 1 = the next vector by
+    DPP, 2 = one unaligned load for 4- and 8-byte elements), bit for bit: the every-offset
+    test above reruns in a child process under each."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.abspath(__file__)
+    r = subprocess.run([sys.executable, "-m", "pytest", here, "-q", "-p", "no:cacheprovider", "-k",
+                        "test_combine_realigned_every_offset"], capture_output=True, text=True, timeout=280,
+                       env=dict(os.environ, SOSX_COMBINE_REALIGN=mode), cwd=os.path.dirname(os.path.dirname(here)))
+    assert r.returncode == 0, (r.stdout[-2500:], r.stderr[-1500:])
+    assert "7 passed" in r.stdout
+
+
 def test_combine3_out_of_place(torch_cuda, sos, oracle):
     torch = torch_cuda
     n = 100003
