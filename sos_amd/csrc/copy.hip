@@ -101,6 +101,7 @@ struct GatherArgs {
     uint64_t tstart[kMaxSeg + 1];  // prefix sums of each segment's tiles
     int nseg;
     int acquire;               // each workgroup acquires before its loads (carry_acquire)
+    int ul;                    // incongruent sources at 4-B offsets: unaligned loads
 };
 
 // A gather whose launch also carries the preceding p2p signalling step: every workgroup
@@ -144,6 +145,12 @@ __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g, Sig<kMaxGate>
             for (int u = 0; u < kGatherU; ++u) {
                 const uint64_t j = j0 + (uint64_t)u * kThreads;
                 if (j < nv) v[u] = __builtin_nontemporal_load(src + j);
+            }
+        } else if (g.ul && (sd & 3) == 0) {  // one unaligned 16-B load per vector
+#pragma unroll
+            for (int u = 0; u < kGatherU; ++u) {
+                const uint64_t j = j0 + (uint64_t)u * kThreads;
+                if (j < nv) v[u] = ldv_unaligned(reinterpret_cast<const char *>(src + j) + sd);
             }
         } else {  // src at another 16-B offset: aligned vectors j and j + 1, funnel-shifted
             // vector j + 1 is the next lane's vector j: taken by DPP (next_lane16), loaded
@@ -194,6 +201,19 @@ __global__ __launch_bounds__(kThreads) void k_gather(GatherArgs g, Sig<kMaxGate>
 using namespace sos;
 
 namespace {
+
+// An incongruent source at a 4-B multiple offset: one unaligned 16-B load per vector
+// (2, the default), 6.20-6.24 TB/s against 6.08-6.11 for the DPP shape and 6.28 congruent
+// (7 x 64 MiB, profiles/r6_gather_realign_ab.txt); other offsets keep DPP.  Bench switch
+// SOSX_GATHER_REALIGN=0: DPP for every offset.
+inline int gather_realign_mode()
+{
+    static const int m = [] {
+        const char *e = getenv("SOSX_GATHER_REALIGN");
+        return e && *e ? atoi(e) : 2;
+    }();
+    return m;
+}
 
 // A gate's signalling step as its own one-workgroup launch.
 int launch_step(const Sig<kMaxGate> &gate, hipStream_t st)
@@ -264,6 +284,7 @@ int gather_impl(int nseg, const void *const *srcs, void *const *dsts, const size
         if (!n) continue;
         g.nseg = n;
         g.tstart[n] = tot;
+        g.ul = gather_realign_mode() == 2;
         const uint64_t blocks = tot ? tot : 1;  // one tile per workgroup (+ the ragged ends)
         if (blocks > 0xffffffffull) return SOSX_ERR_ARG;
         Sig<kMaxGate> none;

@@ -282,13 +282,15 @@ def test_loopback_reduce_twelve_pes(torch_cuda, alg):
             assert np.array_equal(bits(got[p]), bits(ref[p])), (alg, n, p)
 
 
-@pytest.mark.parametrize("case", ["allgather8", "ragged", "incongruent", "incongruent_many", "many", "tiny"])
+@pytest.mark.parametrize("case", ["allgather8", "ragged", "incongruent", "incongruent_word", "incongruent_many",
+                                  "many", "tiny"])
 def test_gather_kernel(torch_cuda, case):
     """sosx_gather (the p2p transport's multi-segment copy, copy.hip k_gather): one tile
     per workgroup over the 16-B bodies on the destination's grid (a source at another 16-B
-    offset realigned in registers), byte loops for the ragged ends; more than 16 segments
-    split into several launches.  Every destination byte must equal its source byte, and
-    bytes around the segments stay untouched."""
+    offset: unaligned loads at 4-B multiples, realigned in registers otherwise), byte loops
+    for the ragged ends; more than 16 segments split into several launches.  Every
+    destination byte must equal its source byte, and bytes around the segments stay
+    untouched."""
     import ctypes
     torch = torch_cuda
     rng = np.random.default_rng(7)
@@ -298,6 +300,8 @@ def test_gather_kernel(torch_cuda, case):
         segs = [(3, 3, 1000003), (16, 16, 65536 + 5), (1, 1, 17), (8, 8, 4096 * 16 + 1)]
     elif case == "incongruent":
         segs = [(1, 2, 100000), (5, 0, 33), (0, 7, 70000)]
+    elif case == "incongruent_word":  # sources at 4 / 8 / 12 B from the destination's grid
+        segs = [(4, 0, 1000003), (0, 8, 65536 + 9), (13, 1, 300001), (7, 3, 4096 * 64 + 2), (2, 6, 33)]
     elif case == "many":
         segs = [(int(rng.integers(0, 16)),) * 2 + (int(rng.integers(1, 200000)),) for _ in range(37)]
     elif case == "incongruent_many":  # every src/dst offset pair, bodies realigned in registers
@@ -322,6 +326,19 @@ def test_gather_kernel(torch_cuda, case):
     for (s, so, n), (d, do, _) in zip(srcs, dsts):
         assert torch.equal(d[do:do + n], s[so:so + n])
         assert bool((d[:do] == 0xA5).all()) and bool((d[do + n:] == 0xA5).all())
+
+
+def test_gather_dpp_shape_forced():
+    """SOSX_GATHER_REALIGN=0 (every incongruent source by the DPP shape, the default only
+    for offsets that are not 4-B multiples): the gather cases above rerun in a child."""
+    import subprocess
+    import sys
+    here = os.path.abspath(__file__)
+    r = subprocess.run([sys.executable, "-m", "pytest", here, "-q", "-p", "no:cacheprovider", "-k",
+                        "test_gather_kernel"], capture_output=True, text=True, timeout=200,
+                       env=dict(os.environ, SOSX_GATHER_REALIGN="0"), cwd=os.path.dirname(os.path.dirname(here)))
+    assert r.returncode == 0, (r.stdout[-2500:], r.stderr[-1500:])
+    assert "7 passed" in r.stdout
 
 
 def _perspective_inputs(dt, P, n, seed):
