@@ -14,8 +14,10 @@
 //      post every send;
 //   2. for every receive: wait for the peer's post, locate the bytes from the peer's
 //      own plan (built here: plans are deterministic) and its published offsets; then
-//      a system-scope acquire in stream order (the acquire kernel), so no launch below
-//      reads a line this GPU's L2s kept from an earlier call;
+//      a system-scope acquire in stream order -- carried by the consuming launches' own
+//      workgroups when their grids are small, else the acquire kernel first (carry.h) --
+//      so no launch below reads a line this GPU's L2s kept from an earlier call
+//      (DESIGN.md section 7.3);
 //   3. folds whose inputs are received chunks read them IN PLACE from peer memory
 //      (no staging copy) -- allowed when the round's outputs do not overlap the
 //      bytes this PE is sending in the same round; the other receives are copied by
@@ -30,9 +32,10 @@
 //   stream (the default): between rounds the counters move in stream
 //     order, written and awaited by a one-workgroup kernel (sosx_p2p_signal) on
 //     host-registered node shared memory, so the rounds are enqueued back to back and
-//     the host synchronises once; a step that awaited posts is followed by the acquire
-//     kernel (a small gather that carries the step acquires in each workgroup).  The call's entry and exit boundaries stay on the
-//     host (there is nothing queued for a signal kernel to overlap there).  Each PE's buffer offsets for the
+//     the host synchronises once; the launches after a step that awaited posts owe the
+//     acquire (a small gather that carries the step acquires in each workgroup).  The
+//     call's entry and exit boundaries stay on the host (there is nothing queued for a
+//     signal kernel to overlap there).  Each PE's buffer offsets for the
 //     call travel ahead of the data through a small descriptor ring per ordered pair
 //     (host handshake only, never waiting on a GPU).
 //   host (SHMEMX_P2P_SIGNAL=host, or when HIP cannot register the segment): the host
