@@ -21,8 +21,12 @@
 // the backend classifies every wait (a `posted` / `dposted` counter: a peer's bytes) and
 // every queued copy or fold (does it read another PE's heap?) on its own, and a peer read
 // with a wait since the protocol's last acquire() ends the run ("peer read without an
-// acquire").  Build with -DBROKEN_ACQUIRE to drop the acquires: the run must then fail
-// that way (the negative control).
+// acquire").  As in the HIP backend (sos_amd/csrc/carry.h), acquire() only marks the
+// acquire owed and the next peer-reading launch pays it: carried in its own workgroups
+// (the acquire stays owed for the launches after it) or as the stream-wide kernel first
+// (settled); here the choice is a per-launch coin instead of the grid size, so both forms
+// and their mixtures within one round are exercised.  Build with -DBROKEN_ACQUIRE to drop
+// the acquires: the run must then fail that way (the negative control).
 //
 // Stream mode runs with the entry boundary on the host, queued, and mixed across PEs.
 //
@@ -111,7 +115,7 @@ bool in_peer_heap(int me, const void *p)
     return false;
 }
 
-std::atomic<long> g_acquires{0}, g_peer_reads{0};
+std::atomic<long> g_acquires{0}, g_peer_reads{0}, g_carried{0}, g_stream_wide{0};
 
 struct CpuBackend {
     Stream *s;
@@ -119,6 +123,8 @@ struct CpuBackend {
     int me;
     sosp2p::Shared *sh;
     sosp2p::AcquireTrack trk;
+    bool owed = false;       // carry.h `want`: acquire() ran, no stream-wide acquire since
+    uint64_t coin = 0x9E3779B97F4A7C15ull;
     void read(bool own)
     {
         trk.read(own);
@@ -126,12 +132,32 @@ struct CpuBackend {
         if (own) g_acquires++;
         if (trk.unacquired) die("peer read without an acquire", me);
     }
+    // a launch that reads a peer's heap, as HipBackend::peer_launch + carry_acquire
+    void peer_launch_read()
+    {
+        if (!owed) {
+            read(false);
+            return;
+        }
+        coin ^= coin << 13;
+        coin ^= coin >> 7;
+        coin ^= coin << 17;
+        if (coin & 1) {  // a small grid: each workgroup acquires; still owed afterwards
+            g_carried++;
+            read(true);
+        } else {  // a streaming grid: the acquire kernel first, which settles it
+            owed = false;
+            trk.acquired();
+            g_acquires++;
+            g_stream_wide++;
+            s->push([] { std::atomic_thread_fence(std::memory_order_acquire); });
+            read(false);
+        }
+    }
     int acquire()
     {
 #ifndef BROKEN_ACQUIRE
-        trk.acquired();
-        g_acquires++;
-        s->push([] { std::atomic_thread_fence(std::memory_order_acquire); });
+        owed = true;
 #endif
         return 0;
     }
@@ -157,7 +183,7 @@ struct CpuBackend {
     {
         bool peer = false;
         for (int i = 0; i < n; ++i) peer |= in_peer_heap(me, srcs[i]);
-        if (peer) read(false);
+        if (peer) peer_launch_read();
         std::vector<const void *> sv(srcs, srcs + n);
         std::vector<void *> dv(dsts, dsts + n);
         std::vector<size_t> bv(bytes, bytes + n);
@@ -169,14 +195,12 @@ struct CpuBackend {
     int run_ops(const sosplan::Round &r, const std::vector<std::vector<const void *>> &ins,
                 const sosp2p::LocalPtr &local_ptr)
     {
-        for (const auto &in : ins) {
-            bool peer = false;
-            for (const void *p : in) peer |= in_peer_heap(me, p);
-            if (peer) read(false);
-        }
         for (size_t i = 0; i < r.ops.size(); ++i) {
             const sosplan::Local l = r.ops[i];
             const std::vector<const void *> in = ins[i];
+            bool peer = false;
+            for (const void *p : in) peer |= in_peer_heap(me, p);
+            if (peer) peer_launch_read();
             if (l.kind == sosplan::COPY) {
                 char *o = local_ptr(l.out_buf, l.out_off);
                 s->push([o, in, l] { if (o != in[0]) memmove(o, in[0], l.count); });
@@ -246,7 +270,10 @@ struct CpuBackend {
         signal(nw, wa, wv, nq, qa, qv);
         bool peer = false;
         for (int i = 0; i < n; ++i) peer |= in_peer_heap(me, srcs[i]);
-        if (peer) read(own);
+        if (peer) {
+            if (own) read(true);
+            else peer_launch_read();
+        }
         std::vector<const void *> sv(srcs, srcs + n);
         std::vector<void *> dv(dsts, dsts + n);
         std::vector<size_t> bv(bytes, bytes + n);
@@ -409,8 +436,12 @@ int main(int argc, char **argv)
     }
     free(sh);
     if (g_peer_reads.load() == 0) die("no launch read a peer's bytes");
+#ifndef BROKEN_ACQUIRE
+    if (g_carried.load() == 0 || g_stream_wide.load() == 0) die("one form of the acquire never ran");
+#endif
     printf("p2p protocol harness: %ld calls OK (host and stream signalling, both entries); "
-           "%ld peer reads, each after an acquire (%ld acquires)\n", total, g_peer_reads.load(),
-           g_acquires.load());
+           "%ld peer reads, each after an acquire (%ld acquires: %ld carried by the launch, %ld "
+           "stream-wide)\n", total, g_peer_reads.load(), g_acquires.load(), g_carried.load(),
+           g_stream_wide.load());
     return 0;
 }
