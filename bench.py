@@ -592,6 +592,9 @@ MALL_BYTES = 256 << 20         # MI355X Infinity Cache (MALL), chip total
 ROTATE_BYTES = 1 << 30         # operand bytes a rotation cycles through per size point
 
 
+GRAPH_MAX_BYTES = 64 << 20  # graph-replayed curve points: 1Mi..16Mi fp32
+
+
 def time_launches(torch, stream, launches, reps):
     """Mean HIP-event time per launch of `reps` back-to-back calls of launches[i % len]."""
     for k in range(min(3, len(launches))):
@@ -604,6 +607,35 @@ def time_launches(torch, stream, launches, reps):
     s1.record(stream)
     torch.cuda.synchronize()
     return s0.elapsed_time(s1) / 1e3 / reps
+
+
+def time_graph(torch, launch_on, ntargets, reps):
+    """Mean time per launch of `reps` launches (target i % ntargets) captured into one HIP
+    graph and replayed: the GPU runs them back to back with no host enqueue in between, so
+    small sizes show the kernel and its dispatch gap rather than the host's launch rate.
+    None if the capture fails."""
+    try:
+        side = torch.cuda.Stream()
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=side):
+            h = torch.cuda.current_stream().cuda_stream
+            for r in range(reps):
+                launch_on(r % ntargets, h)
+        with torch.cuda.stream(side):  # replay() launches on the current stream
+            g.replay()
+            torch.cuda.synchronize()
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record(side)
+            g.replay()
+            s1.record(side)
+        torch.cuda.synchronize()
+        t = s0.elapsed_time(s1) / 1e3 / reps
+        del g
+        return t
+    except Exception as e:  # noqa: BLE001 -- the eager figure stands alone then
+        log(f"[curve] graph capture failed: {e}")
+        return None
 
 
 def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
@@ -646,6 +678,8 @@ def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
         reps = max(10, min(400, int(4e9 // (3 * nb))), 2 * npairs)
         kern = time_launches(torch, stream, launches, reps)
         resident = time_launches(torch, stream, launches[:1], max(10, min(200, int(4e9 // (3 * nb)))))
+        graph = time_graph(torch, lambda i, h: L.combine(op, dt, bufs[i][0].ptr, bufs[i][1].ptr, m, h),
+                           len(bufs), reps) if nb <= GRAPH_MAX_BYTES else None
         del launches
         for a, b in bufs:
             a.free()
@@ -659,6 +693,9 @@ def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
                "resident_kernel_us": round(resident * 1e6, 2),
                "resident_GBs": round(algo / resident / 1e9, 1),
                "cache_resident": algo <= MALL_BYTES}
+        if graph:
+            row.update({"graph_kernel_us": round(graph * 1e6, 2), "graph_GBs": round(algo / graph / 1e9, 1),
+                        "graph_frac_hbm": round(algo / graph / 1e9 / HBM_PEAK_GBS, 4)})
         if O is not None:
             inout = O.fill(dt, dist, SEED, 0, m)
             inp = O.fill(dt, dist, SEED, 1, m)
@@ -677,7 +714,9 @@ def size_curve_n1(args, torch, cpu=True, cpu_seconds=1.0):
             "gpu": ("mean HIP-event kernel time over a batch of back-to-back launches; kernel_us / "
                     "GBs / frac_hbm with the launches rotating over operand pairs of >= 1 GiB in "
                     "all (HBM-streamed), resident_* on one pair (cache_resident: the three "
-                    "streams fit the 256 MiB Infinity Cache, not an HBM figure)"),
+                    "streams fit the 256 MiB Infinity Cache, not an HBM figure); graph_* (up to "
+                    "16Mi): the same rotating batch captured in one HIP graph and replayed, so the "
+                    "host's launch rate does not bound the small sizes"),
             "cpu": (f"oracle/sos_oracle.c reduce_local (SOS's loop, gcc -O2), 1 thread, "
                     f"~{cpu_seconds:g} s per point, same inputs" if cpu else "skipped"),
             "rows": rows}
