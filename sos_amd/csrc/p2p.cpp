@@ -192,10 +192,12 @@ void spin_until_u64(const uint64_t *a, uint64_t want, const char *what)
 }
 
 // SOSX_P2P_TRACE=N (diagnostics): host time per phase of p2p_exec, averaged and printed
-// to stderr every N calls.
+// to stderr every N calls, with the host time spent inside the backend's release, signal,
+// gather and local-op calls (the launches themselves).
 struct Trace {
     int every = -1;  // -1: not read yet, 0: off
     double t[6] = {0, 0, 0, 0, 0, 0};
+    double b[4] = {0, 0, 0, 0};  // host time inside the backend: release, signal, gather, ops
     long calls = 0;
 };
 Trace g_trace;
@@ -415,7 +417,19 @@ struct HipBackend {
     bool tr;
     int complete() { return sosrt::complete(stream) == hipSuccess ? 0 : 1; }
     int drain() { return hipStreamSynchronize(stream) == hipSuccess ? 0 : 1; }
-    int release() { return release_system(stream) == hipSuccess ? 0 : 1; }
+    // host time of one backend call into the trace (SOSX_P2P_TRACE)
+    template <class F> int timed(int slot, F &&f)
+    {
+        if (!tr) return f();
+        const double t0 = now_s();
+        const int rc = f();
+        g_trace.b[slot] += now_s() - t0;
+        return rc;
+    }
+    int release()
+    {
+        return timed(0, [&] { return release_system(stream) == hipSuccess ? 0 : 1; });
+    }
     int acquire()
     {
 #ifdef SOSX_TEST_HOOKS
@@ -452,7 +466,7 @@ struct HipBackend {
         bool peer = false;
         for (int i = 0; i < n; ++i) peer |= in_peer_heap(srcs[i]);
         prof_mark(1, false, stream);
-        const int rc = peer_launch(peer, [&] { return sosx_gather(n, srcs, dsts, bytes, stream); });
+        const int rc = timed(2, [&] { return peer_launch(peer, [&] { return sosx_gather(n, srcs, dsts, bytes, stream); }); });
         prof_mark(1, true, stream);
         return rc;
     }
@@ -460,8 +474,10 @@ struct HipBackend {
                const uint64_t *qv)
     {
         if (device_data_wait(nq, qa)) note_peer_wait();
-        return sosx_p2p_signal(nw, wa, wv, nq, qa, qv, dev(&shared()->sig_err[my_world]),
-                               g_sig.limit_ticks, stream);
+        return timed(1, [&] {
+            return sosx_p2p_signal(nw, wa, wv, nq, qa, qv, dev(&shared()->sig_err[my_world]), g_sig.limit_ticks,
+                                   stream);
+        });
     }
     int gather_signalled(int n, const void *const *srcs, void *const *dsts, const size_t *bytes, int nw,
                          uint64_t *const *wa, const uint64_t *wv, int nq, const uint64_t *const *qa,
@@ -475,9 +491,11 @@ struct HipBackend {
         bool peer = false;
         for (int i = 0; i < n; ++i) peer |= in_peer_heap(srcs[i]);
         prof_mark(1, false, stream);
-        const int rc = peer_launch(peer, [&] {
-            return sosx_gather_signalled(n, srcs, dsts, bytes, nw, wa, wv, nq, qa, qv,
-                                         dev(&shared()->sig_err[my_world]), g_sig.limit_ticks, stream);
+        const int rc = timed(2, [&] {
+            return peer_launch(peer, [&] {
+                return sosx_gather_signalled(n, srcs, dsts, bytes, nw, wa, wv, nq, qa, qv,
+                                             dev(&shared()->sig_err[my_world]), g_sig.limit_ticks, stream);
+            });
         });
         prof_mark(1, true, stream);
         return rc;
@@ -488,7 +506,9 @@ struct HipBackend {
         for (size_t i = 0; i < r.ops.size(); ++i) {
             bool peer = false;
             for (const void *p : ins[i]) peer |= in_peer_heap(p);
-            const int rc = peer_launch(peer, [&] { return run_round_op(r.ops[i], ins[i], local_ptr, op, dt, stream); });
+            const int rc = timed(3, [&] {
+                return peer_launch(peer, [&] { return run_round_op(r.ops[i], ins[i], local_ptr, op, dt, stream); });
+            });
             if (rc) return rc;
         }
         return SOSX_OK;
@@ -544,9 +564,11 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
         if (tr && ++g_trace.calls % g_trace.every == 0) {
             const double k = 1e6 / (double)g_trace.every;
             fprintf(stderr, "[%04d] p2p trace, stream mode (calls %ld-%ld, us/call): descriptors %.1f "
-                    "enqueue %.1f sync-end %.1f\n", s.my_pe, g_trace.calls - g_trace.every + 1,
-                    g_trace.calls, g_trace.t[1] * k, g_trace.t[2] * k, g_trace.t[5] * k);
+                    "enqueue %.1f (release %.1f signal %.1f gather %.1f ops %.1f) sync-end %.1f\n", s.my_pe,
+                    g_trace.calls - g_trace.every + 1, g_trace.calls, g_trace.t[1] * k, g_trace.t[2] * k,
+                    g_trace.b[0] * k, g_trace.b[1] * k, g_trace.b[2] * k, g_trace.b[3] * k, g_trace.t[5] * k);
             for (double &v : g_trace.t) v = 0;
+            for (double &v : g_trace.b) v = 0;
         }
         return rc;
     }
@@ -554,10 +576,12 @@ int p2p_exec(const sosplan::Plan &plan, const Team &t, int alg, uint64_t count, 
     if (tr && ++g_trace.calls % g_trace.every == 0) {  // window averages, then reset
         const double k = 1e6 / (double)g_trace.every;
         fprintf(stderr, "[%04d] p2p trace (calls %ld-%ld, us/call): sync-send %.1f wait-post %.1f "
-                "enqueue %.1f sync-ops %.1f wait-consumed %.1f sync-end %.1f\n", s.my_pe,
+                "enqueue %.1f (gather %.1f ops %.1f) sync-ops %.1f wait-consumed %.1f sync-end %.1f\n", s.my_pe,
                 g_trace.calls - g_trace.every + 1, g_trace.calls, g_trace.t[0] * k, g_trace.t[1] * k,
-                g_trace.t[2] * k, g_trace.t[3] * k, g_trace.t[4] * k, g_trace.t[5] * k);
+                g_trace.t[2] * k, g_trace.b[2] * k, g_trace.b[3] * k, g_trace.t[3] * k, g_trace.t[4] * k,
+                g_trace.t[5] * k);
         for (double &v : g_trace.t) v = 0;
+        for (double &v : g_trace.b) v = 0;
     }
     return rc;
 }
