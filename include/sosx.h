@@ -284,10 +284,6 @@ int sosx_small_stage(void *dst, const void *src, size_t bytes, uint64_t *const *
 
 long sosx_small_path_calls(void);
 long sosx_small_path_device_calls(void);
-
-/* Of those, calls whose fold awaited the peers' posts on the GPU (a staged device operand:
- * the fold is queued behind the staging kernel instead of launched after a host wait). */
-long sosx_small_path_gated_calls(void);
 /* Limit for device-resident operands on that path: a call takes it when team size *
  * operand bytes <= team_bytes (0: never; default SHMEMX_SMALL_DEVICE, 128 KiB).  Returns
  * the previous limit.  Collective in effect: every PE of a team must hold the same limit

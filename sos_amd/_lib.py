@@ -89,7 +89,6 @@ _SIGS = {
     "sosx_build_info": (_c.c_char_p, []),
     "sosx_small_path_calls": (_c.c_long, []),
     "sosx_small_path_device_calls": (_c.c_long, []),
-    "sosx_small_path_gated_calls": (_c.c_long, []),
     "sosx_small_stage": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_void_p,
                                     _c.c_int, _c.c_void_p]),
     "sosx_set_small_device_bytes": (_c.c_size_t, [_c.c_size_t]),

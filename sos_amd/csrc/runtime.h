@@ -232,7 +232,6 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
                        const Team &t, int op, int dt, const char *fn);
 long small_path_calls();
 long small_path_device_calls();
-long small_path_gated_calls();
 size_t small_path_set_device_bytes(size_t team_bytes);
 // shmemx_reduce_local on operands of <= 64 KiB that are both in HBM or both in host memory:
 // one launch + completion words (smallpath.cpp); false = not taken, use the general path.

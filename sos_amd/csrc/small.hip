@@ -21,7 +21,6 @@
 // slots starts with a system-scope acquire (slot_acquire): lane 0 fences, waits for the
 // invalidate, and the workgroup's loads follow the barrier.
 #include "fold_kernels.h"
-#include "small_gate.h"
 
 namespace sos {
 
@@ -33,41 +32,6 @@ namespace sos {
 // arguments instead of 1 KiB, which the host launch call copies every time
 // (SOSX_SMALL_TRACE measured the launch call at 3.0 us with the 1 KiB block).
 __device__ __forceinline__ void slot_acquire() { wg_acquire(); }
-
-// The device-side wait of a gated call (small_gate.h): lane i < n of every workgroup waits
-// until peer i's post count reaches the call's, bounded by `limit` ticks (expiry sets
-// *err, and an expired or already failed call reads nothing).  True when every post came.
-__device__ __forceinline__ bool small_gate_wait(const SmallGate &g)
-{
-    __shared__ int bad;
-    if (threadIdx.x == 0) bad = 0;
-    __syncthreads();
-    const int i = (int)threadIdx.x;
-    if (i < g.n) {
-        const long long t0 = wall_clock64();
-        while (__hip_atomic_load(g.posted[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < g.want[i]) {
-            if (__hip_atomic_load(g.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
-                wall_clock64() - t0 > g.limit) {
-                __hip_atomic_store(g.err, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                bad = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    __syncthreads();
-    return bad == 0;
-}
-
-// Operand k of a gated call: the peer's slot its post names (written by the peer's host
-// before the post), or p itself.
-__device__ __forceinline__ const void *gate_ptr(const SmallGate &g, int k, const void *p)
-{
-    const int e = g.op_of[k];
-    if (e < 0) return p;
-    const uint32_t id = __hip_atomic_load(g.ring[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return g.base[e] + (size_t)id * g.slot;
-}
 
 template <int MAXP> struct SmallFoldArgsT {
     const void *leaf[MAXP];
@@ -170,19 +134,8 @@ __device__ __forceinline__ void small_fold_lane(T *out, const A &a, size_t n, si
 }
 
 template <class T, class OP, int P2, bool VEC, class A>
-__global__ __launch_bounds__(kThreads) void k_small_fold(T *out, A a, size_t n, SmallGate gate)
+__global__ __launch_bounds__(kThreads) void k_small_fold(T *out, A a, size_t n)
 {
-    if (gate.n) {
-        if (!small_gate_wait(gate)) {
-            signal_done(a.flags, a.seq);
-            return;
-        }
-#pragma unroll
-        for (int y = 0; y < kGateMax; ++y) {
-            a.leaf[y] = gate_ptr(gate, y, a.leaf[y]);
-            a.extra[y] = gate_ptr(gate, kGateMax + y, a.extra[y]);
-        }
-    }
     slot_acquire();
     small_fold_lane<T, OP, P2, VEC, A>(out, a, n, (size_t)blockIdx.x * kThreads + threadIdx.x);
     signal_done(a.flags, a.seq);
@@ -220,16 +173,8 @@ __device__ __forceinline__ T ring_elem(const SmallRingArgs &a, int c, size_t i)
 
 // The same, team size at run time, one element per lane (operands not 16-B aligned).
 template <class T, class OP>
-__global__ __launch_bounds__(kThreads) void k_small_ring_dyn(T *out, SmallRingArgs a, int np, SmallGate gate)
+__global__ __launch_bounds__(kThreads) void k_small_ring_dyn(T *out, SmallRingArgs a, int np)
 {
-    if (gate.n) {
-        if (!small_gate_wait(gate)) {
-            signal_done(a.flags, a.seq);
-            return;
-        }
-#pragma unroll
-        for (int k = 0; k < kGateMax; ++k) a.in[k] = gate_ptr(gate, k, a.in[k]);
-    }
     if (a.acquire) slot_acquire();
     const uint64_t b = blockIdx.x;
     int c = 0;
@@ -248,16 +193,8 @@ __global__ __launch_bounds__(kThreads) void k_small_ring_dyn(T *out, SmallRingAr
 }
 
 template <class T, class OP, int NP, bool VEC>
-__global__ __launch_bounds__(kThreads) void k_small_ring(T *out, SmallRingArgs a, SmallGate gate)
+__global__ __launch_bounds__(kThreads) void k_small_ring(T *out, SmallRingArgs a)
 {
-    if (gate.n) {
-        if (!small_gate_wait(gate)) {
-            signal_done(a.flags, a.seq);
-            return;
-        }
-#pragma unroll
-        for (int k = 0; k < kGateMax; ++k) a.in[k] = gate_ptr(gate, k, a.in[k]);
-    }
     if (a.acquire) slot_acquire();
     const uint64_t b = blockIdx.x;
     int c = 0;
@@ -341,8 +278,7 @@ namespace {
 
 struct SmallFoldFn {
     template <class T, class OP>
-    static int run(void *out, const SmallFoldArgs *a, size_t n, bool vec, unsigned blocks, const SmallGate *gate,
-                   hipStream_t st)
+    static int run(void *out, const SmallFoldArgs *a, size_t n, bool vec, unsigned blocks, hipStream_t st)
     {
         SmallFoldArgs8 a8;
         memset(&a8, 0, sizeof(a8));
@@ -361,10 +297,10 @@ struct SmallFoldFn {
     case P2:                                                                                       \
         if (vec)                                                                                   \
             hipLaunchKernelGGL((k_small_fold<T, OP, P2, true, SmallFoldArgs8>), dim3(blocks),       \
-                               dim3(kThreads), 0, st, (T *)out, a8, n, *gate);                     \
+                               dim3(kThreads), 0, st, (T *)out, a8, n);                            \
         else  /* unaligned operands: one element per lane, leaf count at run time */             \
             hipLaunchKernelGGL((k_small_fold<T, OP, 0, false, SmallFoldArgs8>), dim3(blocks),       \
-                               dim3(kThreads), 0, st, (T *)out, a8, n, *gate);                     \
+                               dim3(kThreads), 0, st, (T *)out, a8, n);                            \
         break;
             SOS_SMALL(1)
             SOS_SMALL(2)
@@ -373,7 +309,7 @@ struct SmallFoldFn {
 #undef SOS_SMALL
             default:
                 hipLaunchKernelGGL((k_small_fold<T, OP, 0, false, SmallFoldArgs>), dim3(blocks),
-                                   dim3(kThreads), 0, st, (T *)out, *a, n, *gate);
+                                   dim3(kThreads), 0, st, (T *)out, *a, n);
         }
         return hip_ok(hipGetLastError());
     }
@@ -381,20 +317,18 @@ struct SmallFoldFn {
 
 struct SmallRingFn {
     template <class T, class OP>
-    static int run(void *out, const SmallRingArgs *a, int np, bool vec, unsigned blocks, const SmallGate *gate,
-                   hipStream_t st)
+    static int run(void *out, const SmallRingArgs *a, int np, bool vec, unsigned blocks, hipStream_t st)
     {
         if (!vec) {  // unaligned operands: one element per lane, team size at run time
             if (np < 1 || np > 8) return SOSX_ERR_ARG;
-            hipLaunchKernelGGL((k_small_ring_dyn<T, OP>), dim3(blocks), dim3(kThreads), 0, st, (T *)out, *a, np,
-                               *gate);
+            hipLaunchKernelGGL((k_small_ring_dyn<T, OP>), dim3(blocks), dim3(kThreads), 0, st, (T *)out, *a, np);
             return hip_ok(hipGetLastError());
         }
         switch (np) {
 #define SOS_RING(NP)                                                                               \
     case NP:                                                                                       \
         hipLaunchKernelGGL((k_small_ring<T, OP, NP, true>), dim3(blocks), dim3(kThreads), 0, st,     \
-                           (T *)out, *a, *gate);                                                   \
+                           (T *)out, *a);                                                          \
         break;
             SOS_RING(1)
             SOS_RING(2)
@@ -414,24 +348,20 @@ struct SmallRingFn {
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
-const SmallGate kNoGate = {};
-
 }  // namespace
 
-namespace sos {
+extern "C" {
 
 // One PE's recdbl_sw value over p2 leaves (leaves[y], each folded first with extras[y]
 // when that is not null), written to `out`; workgroup b then stores `seq` into flags[b]
 // (pinned host memory), b < *nblocks.  count <= SOSX_SMALL_FOLD_MAX.
-int small_fold_gated(int op, int dtype, void *out, const void *const *leaves, const void *const *extras,
-                     int p2, size_t count, uint32_t *flags, uint32_t seq, int *nblocks, const SmallGate *gate,
-                     void *stream)
+int sosx_small_fold(int op, int dtype, void *out, const void *const *leaves,
+                    const void *const *extras, int p2, size_t count, uint32_t *flags, uint32_t seq,
+                    int *nblocks, void *stream)
 {
     if (p2 < 1 || p2 > SOSX_MAX_FOLD || (p2 & (p2 - 1)) || count > SOSX_SMALL_FOLD_MAX || !flags ||
         !nblocks)
         return SOSX_ERR_ARG;
-    if (!gate) gate = &kNoGate;
-    if (gate->n < 0 || gate->n > kGateMax || (gate->n && (p2 > kGateMax || !gate->err))) return SOSX_ERR_ARG;
     int rc = sos_check_op(op, dtype);
     if (rc) return rc;
     *nblocks = 0;
@@ -454,19 +384,17 @@ int small_fold_gated(int op, int dtype, void *out, const void *const *leaves, co
     const size_t lanes = (count + V - 1) / V;
     const unsigned blocks = (unsigned)((lanes + kThreads - 1) / kThreads);
     *nblocks = (int)blocks;
-    return dispatch<SmallFoldFn>(op, dtype, out, (const SmallFoldArgs *)&a, count, vec, blocks, gate,
+    return dispatch<SmallFoldFn>(op, dtype, out, (const SmallFoldArgs *)&a, count, vec, blocks,
                                  as_stream(stream));
 }
 
 // Every element's SOS ring value for one PE (np = 2..8 team operands in team order),
 // written to `out` (count elements); workgroup b then stores `seq` into flags[b],
 // b < *nblocks.
-int small_ring_gated(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
-                     uint32_t *flags, uint32_t seq, int *nblocks, const SmallGate *gate, void *stream)
+int sosx_small_ring(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
+                    uint32_t *flags, uint32_t seq, int *nblocks, void *stream)
 {
     if (np < 2 || np > 8 || count > SOSX_SMALL_FOLD_MAX || !flags || !nblocks) return SOSX_ERR_ARG;
-    if (!gate) gate = &kNoGate;
-    if (gate->n < 0 || gate->n > kGateMax || (gate->n && !gate->err)) return SOSX_ERR_ARG;
     int rc = sos_check_op(op, dtype);
     if (rc) return rc;
     *nblocks = 0;
@@ -505,7 +433,7 @@ int small_ring_gated(int op, int dtype, void *out, const void *const *ins, int n
     a.vec_out = aligned16(out);
     a.acquire = 1;
     *nblocks = (int)tiles;
-    return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles, gate,
+    return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles,
                                  as_stream(stream));
 }
 
@@ -515,13 +443,10 @@ int small_ring_gated(int op, int dtype, void *out, const void *const *ins, int n
 // the ring kernel with a single chunk: every workgroup folds from ins[0].  acquire != 0:
 // the operands are peers' slots (team calls), each workgroup acquires first; 0 for local
 // operands (shmemx_reduce_local).
-int small_linear_gated(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
-                       uint32_t *flags, uint32_t seq, int *nblocks, int acquire, const SmallGate *gate,
-                       void *stream)
+int sosx_small_linear(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
+                      uint32_t *flags, uint32_t seq, int *nblocks, int acquire, void *stream)
 {
     if (np < 1 || np > 8 || count > SOSX_SMALL_FOLD_MAX || !flags || !nblocks) return SOSX_ERR_ARG;
-    if (!gate) gate = &kNoGate;
-    if (gate->n < 0 || gate->n > kGateMax || (gate->n && !gate->err)) return SOSX_ERR_ARG;
     int rc = sos_check_op(op, dtype);
     if (rc) return rc;
     *nblocks = 0;
@@ -550,30 +475,8 @@ int small_linear_gated(int op, int dtype, void *out, const void *const *ins, int
     a.vec_out = aligned16(out);
     a.acquire = acquire != 0;
     *nblocks = (int)tiles;
-    return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles, gate,
+    return dispatch<SmallRingFn>(op, dtype, out, (const SmallRingArgs *)&a, np, vec, (unsigned)tiles,
                                  as_stream(stream));
-}
-
-}  // namespace sos
-
-extern "C" {
-
-int sosx_small_fold(int op, int dtype, void *out, const void *const *leaves, const void *const *extras, int p2,
-                    size_t count, uint32_t *flags, uint32_t seq, int *nblocks, void *stream)
-{
-    return small_fold_gated(op, dtype, out, leaves, extras, p2, count, flags, seq, nblocks, nullptr, stream);
-}
-
-int sosx_small_ring(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
-                    uint32_t *flags, uint32_t seq, int *nblocks, void *stream)
-{
-    return small_ring_gated(op, dtype, out, ins, np, count, flags, seq, nblocks, nullptr, stream);
-}
-
-int sosx_small_linear(int op, int dtype, void *out, const void *const *ins, int np, size_t count,
-                      uint32_t *flags, uint32_t seq, int *nblocks, int acquire, void *stream)
-{
-    return small_linear_gated(op, dtype, out, ins, np, count, flags, seq, nblocks, acquire, nullptr, stream);
 }
 
 // Copy `bytes` from src (device) to dst (a node-shared slot, device view) in one

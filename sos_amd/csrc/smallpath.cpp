@@ -63,16 +63,9 @@
 
 #include "plan.h"
 #include "runtime.h"
-#include "small_gate.h"
 #include "sosx.h"
 
 namespace sosrt {
-
-using sos::kGateMax;
-using sos::SmallGate;
-using sos::small_fold_gated;
-using sos::small_linear_gated;
-using sos::small_ring_gated;
 
 namespace {
 
@@ -138,11 +131,8 @@ struct Small {
     uint64_t route_k[kMaxPE] = {0};  // this call's index with each team peer (small path)
     uint64_t route_tag = 0;          // this call's route tag
     size_t dev_team_bytes = 0;   // device operands: P * bytes limit (0: host operands only)
-    uint64_t *gate_err = nullptr;  // a gated fold's expired wait (pinned, coherent)
-    long long gate_ticks = 0;      // SHMEMX_P2P_TIMEOUT in device wall-clock ticks
     long calls = 0;
     long dev_calls = 0;          // of which with a device operand
-    long gated_calls = 0;        // of which the fold awaited the peers' posts itself
 };
 Small g;
 
@@ -184,8 +174,7 @@ void wait_ge(const std::atomic<uint64_t> &w, uint64_t v, const char *what)
 // ~12 us, a launch + flag poll ~6.6 us: profiles/r3_sync_probe.json).  Every 4096 polls
 // the stream is queried: an error, or a drained stream whose flags are still missing,
 // ends the job with a message, as does SHMEMX_P2P_TIMEOUT.
-void wait_flags(const uint32_t *flags, int nb, uint32_t seq, const char *fn,
-                const std::function<void()> &poll = nullptr, double margin = 0)
+void wait_flags(const uint32_t *flags, int nb, uint32_t seq, const char *fn)
 {
     const double t0 = now_s();
     unsigned spins = 0;
@@ -196,7 +185,6 @@ void wait_flags(const uint32_t *flags, int nb, uint32_t seq, const char *fn,
         }
         __builtin_ia32_pause();
         if ((++spins & 0xFFF) != 0) continue;
-        if (poll) poll();
         const hipError_t e = hipStreamQuery(st().stream);
         if (e == hipSuccess) {  // drained: every flag must be visible by now (after the
                                 // runtime's own synchronisation at the latest)
@@ -208,20 +196,9 @@ void wait_flags(const uint32_t *flags, int nb, uint32_t seq, const char *fn,
             return;
         }
         if (e != hipErrorNotReady) hip_check(e, fn);
-        if (now_s() - t0 > limit_s() + margin)
+        if (now_s() - t0 > limit_s())
             raise_error("%s: small shared-memory path: timed out after %.0f s", fn, limit_s());
     }
-}
-
-// Bench switch SOSX_SMALL_GATE=0: a staged (device-operand) call waits for the peers'
-// posts on the host before its fold launch, as host-operand calls do.
-bool gate_switch_on()
-{
-    static const bool on = [] {
-        const char *e = getenv("SOSX_SMALL_GATE");
-        return !(e && *e == '0');
-    }();
-    return on;
 }
 
 // SOSX_SMALL_TRACE=N (diagnostics): host time per phase of small_path_reduce, averaged
@@ -283,16 +260,6 @@ void small_path_setup(void *region, size_t bytes)
         ok = 0;
     }
     if (g.flags) memset(g.flags, 0, flag_words * sizeof(uint32_t));
-    int rate_khz = 0;
-    if (ok && hipHostMalloc((void **)&g.gate_err, sizeof(uint64_t), hipHostMallocCoherent) == hipSuccess &&
-        hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, s.device) == hipSuccess && rate_khz > 0) {
-        *g.gate_err = 0;
-        g.gate_ticks = (long long)(limit_s() * 1e3 * (double)rate_khz);
-    } else {  // no device-side waits: the host waits for the peers' posts, as for host operands
-        (void)hipGetLastError();
-        if (g.gate_err) (void)hipHostFree(g.gate_err);
-        g.gate_err = nullptr;
-    }
     std::vector<int> oks((size_t)s.n_pes);
     if (sosboot::hub_allgather(&s.hub, &ok, sizeof(ok), oks.data()) != 0)
         raise_error("shmem_init: small-path agreement failed");
@@ -313,13 +280,11 @@ void small_path_teardown()
     if (g.registered && g.host) (void)hipHostUnregister(g.host);
     if (g.out) (void)hipHostFree(g.out);
     if (g.flags) (void)hipHostFree(g.flags);
-    if (g.gate_err) (void)hipHostFree(g.gate_err);
     g = Small();
 }
 
 long small_path_calls() { return g.calls; }
 long small_path_device_calls() { return g.dev_calls; }
-long small_path_gated_calls() { return g.gated_calls; }
 
 // Collective over the world when the job is up: every PE passes the same limit (checked
 // through the bootstrap), so the path choice for device operands stays uniform.  Without
@@ -542,53 +507,21 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         if (rc) raise_error("%s: small-path copy of a device operand failed (status %d)", fn, rc);
     }
     phase(1);
-    // A staged call's fold is queued right behind the staging kernel and awaits the
-    // peers' posts itself (small_gate.h): the host goes on to the launch instead of a
-    // host<->GPU round trip per peer post.  Only when a launch will read the slots.
-    const bool copy_root = bcast && ((alg - sosplan::PLAN_BCAST) & 1) != 0;
-    const int scan_np = alg == sosplan::PLAN_INSCAN ? me + 1 : me;
-    const int p2 = sosplan::pow2_floor(P), nx = P - p2;
-    const bool reads = bcast ? (me != root || copy_root) : sosplan::is_scan(alg) ? scan_np > 0 : true;
-    const bool fold_alg = !bcast && !sosplan::is_scan(alg) && alg != SOSX_ALG_RING;
-    const bool gate_on = staged && g.gate_err && gate_switch_on() && P - 1 <= kGateMax && reads &&
-                         (!fold_alg || p2 <= kGateMax);
-    SmallGate gate;
-    memset(&gate, 0, sizeof(gate));
-    for (signed char &o : gate.op_of) o = -1;
-    int ent[kMaxPE], gq[kGateMax];
     const void *in[kMaxPE];
     int from[kMaxPE];
     for (int i = 0; i < P; ++i) {
         from[i] = -1;
-        ent[i] = -1;
         const int q = t.world_rank(i);
         if (i == me) {
             in[i] = g.dev + slot_off(mw, sl);
             continue;
         }
         const uint64_t k = ++g.seen_from[q];
-        from[i] = q;
-        if (gate_on) {  // the slot is resolved on the device, after the post
-            const int e = gate.n++;
-            gate.posted[e] = (const uint64_t *)(g.dev + ((char *)&ctl(q)->posted[mw].v - g.host));
-            gate.want[e] = k;
-            gate.ring[e] = (const uint32_t *)(g.dev + ((char *)&ctl(q)->ring[mw][k % 2] - g.host));
-            gate.base[e] = g.dev + slot_off(q, 0);
-            in[i] = gate.base[e];
-            ent[i] = e;
-            gq[e] = q;
-            continue;
-        }
         wait_post(q, k, g.route_tag, fn);
         const int qs = (int)ctl(q)->ring[mw][k % 2];
         in[i] = g.dev + slot_off(q, qs);
+        from[i] = q;
     }
-    if (gate_on) {
-        gate.slot = g.slot;
-        gate.err = g.gate_err;
-        gate.limit = g.gate_ticks;
-    }
-    const SmallGate *gp = gate_on ? &gate : nullptr;
     phase(2);
     // the result goes straight into a device target or the host symmetric heap
     // (device-mapped pinned memory), else into the pinned result slot
@@ -600,20 +533,19 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
         // 3. one launch: the root's bytes into this PE's target -- every non-root, and the
         //    root itself for the team forms (copy_root, src/collectives_c.c4:390-397); the
         //    active-set forms leave the root's target untouched (:342-378)
-        if (me != root || copy_root) {
-            gate.op_of[0] = (signed char)ent[root];
-            rc = small_linear_gated(SOSX_OP_BOR, SOSX_DT_UCHAR, out, &in[root], 1, bytes, g.flags, g.fseq,
-                                    &nblocks, 1, gp, s.stream);
-        } else
+        const bool copy_root = ((alg - sosplan::PLAN_BCAST) & 1) != 0;
+        if (me != root || copy_root)
+            rc = sosx_small_linear(SOSX_OP_BOR, SOSX_DT_UCHAR, out, &in[root], 1, bytes, g.flags,
+                                   g.fseq, &nblocks, 1, s.stream);
+        else
             out = nullptr;  // nothing written: no copy out either
     } else if (sosplan::is_scan(alg)) {
         // 3. one launch: the in-order prefix of the team's sources 0..me (inscan) or
         //    0..me-1 (exscan), the running value the left operand; exscan's PE 0 gets
         //    zeros, as SOS's memset (src/collectives.c:1111-1209)
-        const int np = scan_np;
+        const int np = alg == sosplan::PLAN_INSCAN ? me + 1 : me;
         if (np > 0) {
-            for (int k = 0; k < np && k < kGateMax; ++k) gate.op_of[k] = (signed char)ent[k];
-            rc = small_linear_gated(op, dt, out, in, np, count, g.flags, g.fseq, &nblocks, 1, gp, s.stream);
+            rc = sosx_small_linear(op, dt, out, in, np, count, g.flags, g.fseq, &nblocks, 1, s.stream);
         } else if (dev_dst) {
             hip_check(hipMemsetAsync(out, 0, bytes, s.stream), fn);
             hip_check(sync_system(s.stream), fn);
@@ -623,23 +555,19 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     } else if (alg == SOSX_ALG_RING) {
         // 3. one launch: every ring chunk c folded LINEAR from PE c (the reduce-scatter's
         //    order), all chunks by every PE (the allgather's result)
-        for (int c = 0; c < P && c < kGateMax; ++c) gate.op_of[c] = (signed char)ent[c];
-        rc = small_ring_gated(op, dt, out, in, P, count, g.flags, g.fseq, &nblocks, gp, s.stream);
+        rc = sosx_small_ring(op, dt, out, in, P, count, g.flags, g.fseq, &nblocks, s.stream);
     } else {
         // 3. one launch: this PE's recdbl_sw tree over the leaves w[y] = v[y ^ mp], where
         //    v[x] = in[x] OP in[x + p2] for the extra PEs (x < P - p2), else in[x]
+        const int p2 = sosplan::pow2_floor(P), nx = P - p2;
         const int mp = me < p2 ? me : me - p2;
         const void *leaves[kMaxPE], *extras[kMaxPE];
         for (int y = 0; y < p2; ++y) {
             const int x = y ^ mp;
             leaves[y] = in[x];
             extras[y] = x < nx ? in[x + p2] : nullptr;
-            if (y < kGateMax) {
-                gate.op_of[y] = (signed char)ent[x];
-                gate.op_of[kGateMax + y] = (signed char)(x < nx ? ent[x + p2] : -1);
-            }
         }
-        rc = small_fold_gated(op, dt, out, leaves, extras, p2, count, g.flags, g.fseq, &nblocks, gp, s.stream);
+        rc = sosx_small_fold(op, dt, out, leaves, extras, p2, count, g.flags, g.fseq, &nblocks, s.stream);
     }
     if (rc) raise_error("%s: small-path reduction failed (status %d)", fn, rc);
     // the launch read the peers' slots after their posts, each workgroup behind its own
@@ -650,27 +578,8 @@ void small_path_reduce(int alg, void *target, const void *source, size_t count, 
     if (staged && nblocks == 0) hip_check(sync_system(s.stream), fn);
     phase(3);
     // 4. completion from the workgroups' flags (no stream synchronisation); then the
-    //    peers' slots are read: acknowledge; my result out.  A gated fold's waits run on
-    //    the device: meanwhile the host watches the peers' route words as wait_post does,
-    //    and an expired device wait is reported as the host's own would be.
-    if (gate_on) {
-        double past[kGateMax] = {0};
-        auto expired = [&] {
-            if (__atomic_load_n(g.gate_err, __ATOMIC_ACQUIRE))
-                raise_error("small shared-memory path: timed out after %.0f s waiting for a peer's operand",
-                            limit_s());
-        };
-        wait_flags(g.flags, nblocks, g.fseq, fn, [&] {
-            expired();
-            for (int e = 0; e < gate.n; ++e)
-                if (ctl(gq[e])->posted[mw].v.load(std::memory_order_acquire) < gate.want[e])
-                    route_check(gq[e], gate.want[e], g.route_tag, fn, past[e]);
-        }, 2.0);
-        expired();
-        g.gated_calls++;
-    } else {
-        wait_flags(g.flags, nblocks, g.fseq, fn);
-    }
+    //    peers' slots are read: acknowledge; my result out
+    wait_flags(g.flags, nblocks, g.fseq, fn);
     phase(4);
     for (int i = 0; i < P; ++i)
         if (from[i] >= 0) mine->consumed[from[i]].v.store(g.seen_from[from[i]], std::memory_order_release);
@@ -746,7 +655,6 @@ void small_local_release()
 
 extern "C" long sosx_small_path_calls(void) { return sosrt::small_path_calls(); }
 extern "C" long sosx_small_path_device_calls(void) { return sosrt::small_path_device_calls(); }
-extern "C" long sosx_small_path_gated_calls(void) { return sosrt::small_path_gated_calls(); }
 extern "C" size_t sosx_set_small_device_bytes(size_t team_bytes)
 {
     return sosrt::small_path_set_device_bytes(team_bytes);
