@@ -416,7 +416,23 @@ struct HipBackend {
     double tp;
     bool tr;
     int complete() { return sosrt::complete(stream) == hipSuccess ? 0 : 1; }
-    int drain() { return hipStreamSynchronize(stream) == hipSuccess ? 0 : 1; }
+    bool merge_syncs()
+    {
+#ifdef SOSX_TEST_HOOKS
+        // A/B (test build only, tools/host_sync_ab.sh): every drain and completion separate
+        static const bool separate = [] {
+            const char *e = getenv("SOSX_TEST_SEPARATE_SYNCS");
+            return e && *e == '1';
+        }();
+        return !separate;
+#else
+        return true;
+#endif
+    }
+    int drain(bool release)
+    {
+        return (release ? sosrt::complete(stream) : hipStreamSynchronize(stream)) == hipSuccess ? 0 : 1;
+    }
     // host time of one backend call into the trace (SOSX_P2P_TRACE)
     template <class F> int timed(int slot, F &&f)
     {

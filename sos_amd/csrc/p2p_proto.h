@@ -183,7 +183,9 @@ inline bool round_fusable(const sosplan::Round &r, uint64_t ts, const LocalPtr &
 // Host-signalled executor of one plan at team index `me` of a team whose team index i is
 // world PE world_of(i).  Backend B provides (all on this PE's ordered "stream"):
 //   int complete()        drain the stream, stores in memory (system scope); 0 = ok
-//   int drain()           drain the stream (this PE's reads are done); 0 = ok
+//   int drain(bool release) drain the stream (this PE's reads are done), with a
+//                          system-scope release first when `release` (= complete()); 0 = ok
+//   bool merge_syncs()     let a round's drain serve as the next completion point
 //   int gather(n, srcs, dsts, bytes)                      one multi-segment copy
 //   int run_ops(round, ins, local_ptr)                    the round's local ops
 //   int acquire()          a system-scope acquire in stream order (before peer reads)
@@ -206,12 +208,19 @@ int exec_host(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of,
     LocalPtr local_ptr = [&](int buf, uint64_t off) -> char * {
         return (buf == sosplan::SRC ? (char *)b.src : buf == sosplan::DST ? b.dst : b.scr) + off;
     };
+    // `settled`: the stream is idle and its writes released (complete()) with nothing
+    // enqueued since, so the next completion point needs no second round trip.  A round
+    // whose reads end its stream work completes (release + sync) where it would only
+    // drain, which settles the next round's send boundary or the call's exit.
+    bool settled = false;
+    const bool merge = be.merge_syncs();
     for (const auto &r : plan.rounds) {
         // 1. post sends, once their bytes are final and in memory
         bool any_send = false;
         for (const auto &x : r.xfers) any_send |= x.send != 0;
         if (any_send) {
-            if (be.complete() != 0) return SOSX_ERR_HIP;
+            if (!settled && be.complete() != 0) return SOSX_ERR_HIP;
+            settled = true;
             be.phase(PH_SYNC_SEND);
             for (const auto &x : r.xfers)
                 if (x.send) {
@@ -271,14 +280,21 @@ int exec_host(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of,
         if (!gs.empty()) {
             const int rc = be.gather((int)gs.size(), gs.data(), gd.data(), gb.data());
             if (rc) return rc;
+            settled = false;
         }
         if (fuse_ok) {
             const int rc = be.run_ops(r, ins, local_ptr);
             if (rc) return rc;
+            settled = false;
         }
-        // 4. receives done -> consumed; wait for my sends to be consumed
+        // 4. receives done -> consumed; wait for my sends to be consumed.  With the
+        //    round's ops already queued (fuse_ok) nothing follows on the stream: complete
+        //    instead of draining (one round trip serves the next boundary too)
         be.phase(PH_ENQUEUE);
-        if ((!segs.empty() || fuse_ok) && be.drain() != 0) return SOSX_ERR_HIP;
+        if ((!segs.empty() || fuse_ok) && !settled) {
+            if (be.drain(merge && fuse_ok) != 0) return SOSX_ERR_HIP;
+            settled = merge && fuse_ok;
+        }
         be.phase(PH_SYNC_OPS);
         for (auto &sg : segs) sh->consumed[sg.peer_world][my_world].fetch_add(1, std::memory_order_release);
         for (const auto &x : r.xfers)
@@ -290,9 +306,10 @@ int exec_host(const sosplan::Plan &plan, int P, int me, const WorldOf &world_of,
         if (!fuse_ok) {
             const int rc = be.run_ops(r, ins, local_ptr);
             if (rc) return rc;
+            settled = false;
         }
     }
-    const int e = be.complete();  // the caller's result in memory
+    const int e = settled ? 0 : be.complete();  // the caller's result in memory
     be.phase(PH_SYNC_END);
     return e == 0 ? SOSX_OK : SOSX_ERR_HIP;
 }

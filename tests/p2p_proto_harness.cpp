@@ -172,7 +172,8 @@ struct CpuBackend {
         s->drain();
         return 0;
     }
-    int drain()
+    bool merge_syncs() { return true; }
+    int drain(bool)
     {
 #ifndef BROKEN_DRAIN
         s->drain();
