@@ -85,6 +85,10 @@ def main():
     world = S.team_world()
     dt, op = L.dtype_id("float"), L.op_id("sum")
     S.shmemx_set_reduce_algorithm(L.ALGS[a.alg])
+
+    def oracle_of(ins):  # the schedule the call resolves to at this size (AUTO: ring or recdbl_sw)
+        res = S.lib().sosx_resolve_alg(L.ALGS[a.alg], ins[0].size * 4, 16384)
+        return (O.ring if res == L.ALGS["ring"] else O.recdbl)(op, dt, ins)
     n, n2 = a.n, a.n2
     hsrc = S.shmemx_malloc_device(n * 4)
     hdst = S.shmemx_malloc_device(n * 4)
@@ -101,7 +105,7 @@ def main():
             t1 = O.fill(dt, 0, seed + 3, me, n2)
             L.check(L.lib().sosx_memcpy(hsrc, t1.ctypes.data, n2 * 4, None), "sosx_memcpy")
             fn(world, hdst, hsrc, n2)
-            e1 = O.recdbl(op, dt, [O.fill(dt, 0, seed + 3, q, n2) for q in range(P)])[me]
+            e1 = oracle_of([O.fill(dt, 0, seed + 3, q, n2) for q in range(P)])[me]
             checks += 1
             m1 = int(np.count_nonzero(direct(hdst, n2 * 4).view(np.uint32) != e1.view(np.uint32)))
             if m1:
@@ -110,7 +114,7 @@ def main():
         if me == 0 and it % 10 == 0:
             print(f"[p2p_stress] iteration {it}/{a.iters}", file=sys.stderr, flush=True)
         ins = [O.fill(dt, 0, seed, q, n) for q in range(P)]
-        exp = O.recdbl(op, dt, ins)[me]
+        exp = oracle_of(ins)[me]
         # the expected bytes in device memory for the kernel reader, checked after upload
         L.check(L.lib().sosx_memcpy(hexp, exp.ctypes.data, n * 4, None), "sosx_memcpy")
         assert np.array_equal(direct_pinned(hexp, n * 4), exp.view(np.uint8)), "expected-bytes upload"
@@ -162,7 +166,7 @@ def main():
         L.fill(dt, 0, seed + 7, me, t_in.data_ptr(), n2)
         torch.cuda.synchronize()
         fn(world, t_out.data_ptr(), t_in.data_ptr(), n2)
-        e2 = O.recdbl(op, dt, [O.fill(dt, 0, seed + 7, q, n2) for q in range(P)])[me]
+        e2 = oracle_of([O.fill(dt, 0, seed + 7, q, n2) for q in range(P)])[me]
         got2 = t_out.cpu().numpy().view(np.uint32)
         checks += 1
         m2 = int(np.count_nonzero(got2 != e2.view(np.uint32)))
