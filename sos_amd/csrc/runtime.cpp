@@ -193,6 +193,8 @@ static const EnvDef kEnv[] = {
      "1: integer world reductions as ncclAllReduce; 2: also fp sum/prod (RCCL's order)"},
     {"SHMEMX_P2P_SIGNAL", "string", "stream on one GPU, host across GPUs", "device",
      "p2p round signalling: stream (device) or host"},
+    {"SHMEMX_P2P_ENTRY", "string", "host", "device",
+     "Stream signalling: the call's entry boundary on the host or queued (device)"},
     {"SHMEMX_P2P_TIMEOUT", "long", "300", "device", "Seconds before a p2p wait ends the job"},
     {"SHMEMX_SMALL_HOST", "bool", "true", "device",
      "Small team collectives through node shared memory (host operands; device ones too, below)"},
